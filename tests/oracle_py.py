@@ -1,0 +1,184 @@
+"""tests/oracle_py.py — ctypes view of oracle/build/liboracle.so (TEST INFRASTRUCTURE).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module.  It is the checker: nothing in the product path calls it.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(REPO, "oracle", "build", "liboracle.so")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+_dp = C.POINTER(C.c_double)
+_fp = C.POINTER(C.c_float)
+_ip = C.POINTER(C.c_int32)
+_lp = C.POINTER(C.c_int64)
+
+
+class OrScene(C.Structure):
+    _fields_ = [("n", C.c_int32), ("geom", _dp), ("kind", _ip), ("mat", _dp)]
+
+
+class OrCamera(C.Structure):
+    _fields_ = [(nm, C.c_double * 3) for nm in ("origin", "lower_left_corner", "horizontal", "vertical", "u", "v", "w")] + [
+        ("lens_radius", C.c_double)
+    ]
+
+
+class OrGlibc(C.Structure):
+    _fields_ = [("state", C.c_int32 * 31), ("f", C.c_int32), ("r", C.c_int32), ("draws", C.c_int64)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"oracle not built: {LIB_PATH} (run `make -C oracle`)")
+        L = C.CDLL(LIB_PATH)
+        L.or_glibc_seed.argtypes = [C.POINTER(OrGlibc), C.c_uint32]
+        L.or_glibc_rand.argtypes = [C.POINTER(OrGlibc)]
+        L.or_glibc_rand.restype = C.c_int32
+        L.or_final_scene.argtypes = [C.POINTER(OrGlibc), _dp, _ip, _dp, C.c_int32]
+        L.or_final_scene.restype = C.c_int32
+        L.or_learn_scene.argtypes = [_dp, _ip, _dp, C.c_int32]
+        L.or_learn_scene.restype = C.c_int32
+        L.or_camera_make.argtypes = [C.POINTER(OrCamera), _dp, _dp, _dp, C.c_double, C.c_double, C.c_double, C.c_double]
+        L.or_ref_worker.argtypes = [C.POINTER(OrScene), C.POINTER(OrCamera)] + [C.c_int32] * 6 + [C.POINTER(OrGlibc), _dp]
+        L.or_ref_worker.restype = C.c_int64
+        L.or_ref_kat.argtypes = [C.POINTER(OrScene), C.POINTER(OrCamera)] + [C.c_int32] * 5 + [C.c_uint32, _dp]
+        L.or_ref_kat.restype = C.c_int32
+        L.or_ref_sphere_hit.argtypes = [_dp, C.c_double, _dp, _dp, C.c_double, C.c_double, _dp, _dp, _dp, _ip]
+        L.or_ref_sphere_hit.restype = C.c_int32
+        L.or_ref_refract.argtypes = [_dp, _dp, C.c_double, _dp]
+        L.or_ref_reflect.argtypes = [_dp, _dp, _dp]
+        L.or_ref_reflectance.argtypes = [C.c_double, C.c_double]
+        L.or_ref_reflectance.restype = C.c_double
+        L.or_ref_near_zero.argtypes = [_dp]
+        L.or_ref_near_zero.restype = C.c_int32
+        L.or_ref_scatter.argtypes = [C.c_int32, _dp, _dp, _dp, _dp, C.c_int32, C.c_uint32, _dp, _dp, _dp, _ip]
+        L.or_ref_scatter.restype = C.c_int32
+        fast_args = [C.POINTER(OrScene), C.POINTER(OrCamera)] + [C.c_int32] * 4 + [C.c_uint64] + [C.c_int32] * 3
+        L.or_fast_render.argtypes = fast_args + [_fp]
+        L.or_fast_render.restype = C.c_int32
+        L.or_fast_render_fixed.argtypes = fast_args + [_lp]
+        L.or_fast_render_fixed.restype = C.c_int32
+        L.or_fast_segments.argtypes = fast_args
+        L.or_fast_segments.restype = C.c_int64
+        L.or_fast_sample.argtypes = [C.POINTER(OrScene), C.POINTER(OrCamera)] + [C.c_int32] * 3 + [C.c_uint64] + [C.c_int32] * 3 + [_fp]
+        L.or_fast_sample.restype = C.c_int32
+        L.or_fast_rng.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_int32, C.POINTER(C.c_uint64)]
+        _lib = L
+    return _lib
+
+
+def dptr(a):
+    return a.ctypes.data_as(_dp)
+
+
+class Scene:
+    """Flat scene arrays (geom 4n, kind n, mat 4n) + the ctypes struct."""
+
+    def __init__(self, geom, kind, mat):
+        self.geom = np.ascontiguousarray(geom, dtype=np.float64).reshape(-1)
+        self.kind = np.ascontiguousarray(kind, dtype=np.int32).reshape(-1)
+        self.mat = np.ascontiguousarray(mat, dtype=np.float64).reshape(-1)
+        self.n = self.kind.size
+        self.c = OrScene(self.n, dptr(self.geom), self.kind.ctypes.data_as(_ip), dptr(self.mat))
+
+
+def final_scene():
+    """random_scene() from the seed-1 stream; returns (Scene, stream after it)."""
+    g = OrGlibc()
+    lib().or_glibc_seed(C.byref(g), 1)
+    geom = np.zeros(4 * 600)
+    kind = np.zeros(600, np.int32)
+    mat = np.zeros(4 * 600)
+    n = lib().or_final_scene(C.byref(g), dptr(geom), kind.ctypes.data_as(_ip), dptr(mat), 600)
+    return Scene(geom[: 4 * n], kind[:n], mat[: 4 * n]), g
+
+
+def learn_scene():
+    geom = np.zeros(20)
+    kind = np.zeros(5, np.int32)
+    mat = np.zeros(20)
+    lib().or_learn_scene(dptr(geom), kind.ctypes.data_as(_ip), dptr(mat), 5)
+    return Scene(geom, kind, mat)
+
+
+def make_camera(lookfrom, lookat, vup, vfov, aspect, aperture, focus):
+    c = OrCamera()
+    a = [np.asarray(x, dtype=np.float64) for x in (lookfrom, lookat, vup)]
+    lib().or_camera_make(C.byref(c), dptr(a[0]), dptr(a[1]), dptr(a[2]), vfov, aspect, aperture, focus)
+    return c
+
+
+def final_camera(aspect=1.5):
+    return make_camera((13, 2, 3), (0, 0, 0), (0, 1, 0), 20.0, aspect, 0.1, 10.0)
+
+
+def learn_camera(aspect=16.0 / 9.0):
+    lf, la = np.array([3.0, 3, 2]), np.array([0.0, 0, -1])
+    d = lf - la
+    focus = float(np.sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]))
+    return make_camera(lf, la, (0, 1, 0), 20.0, aspect, 0.5, focus)
+
+
+def camera_dict(c):
+    return {nm: list(getattr(c, nm)) for nm in ("origin", "lower_left_corner", "horizontal", "vertical", "u", "v", "w")} | {
+        "lens_radius": c.lens_radius
+    }
+
+
+def ref_worker(scene, cam, W, H, spp, depth, start, end, g):
+    out = np.zeros((end - start) * 3)
+    draws = lib().or_ref_worker(C.byref(scene.c), C.byref(cam), W, H, spp, depth, start, end, C.byref(g), dptr(out))
+    return out, draws
+
+
+def ref_kat(scene, cam, W, H, depth, i, j, seed):
+    out = np.zeros(3)
+    nxt = lib().or_ref_kat(C.byref(scene.c), C.byref(cam), W, H, depth, i, j, seed, dptr(out))
+    return out, nxt
+
+
+def fast_render(scene, cam, W, H, spp, depth, seed, row0=0, row_step=1, nrows=None, fixed=False):
+    nrows = H if nrows is None else nrows
+    if fixed:
+        out = np.zeros(nrows * W * 3, np.int64)
+        rc = lib().or_fast_render_fixed(C.byref(scene.c), C.byref(cam), W, H, spp, depth, seed, row0, row_step, nrows, out.ctypes.data_as(_lp))
+    else:
+        out = np.zeros(nrows * W * 3, np.float32)
+        rc = lib().or_fast_render(C.byref(scene.c), C.byref(cam), W, H, spp, depth, seed, row0, row_step, nrows, out.ctypes.data_as(_fp))
+    if rc != 0:
+        raise ValueError("or_fast_render failed")
+    return out.reshape(nrows, W, 3)
+
+
+def fast_segments(scene, cam, W, H, spp, depth, seed, row0=0, row_step=1, nrows=None):
+    nrows = H if nrows is None else nrows
+    return lib().or_fast_segments(C.byref(scene.c), C.byref(cam), W, H, spp, depth, seed, row0, row_step, nrows)
+
+
+def load_scene_txt(path):
+    rows = open(path).read().split("\n")
+    n = int(rows[0])
+    data = [r.split() for r in rows[1 : 1 + n]]
+    geom = np.array([[float(x) for x in r[:4]] for r in data])
+    kind = np.array([int(r[4]) for r in data], np.int32)
+    mat = np.array([[float(x) for x in r[5:9]] for r in data])
+    return Scene(geom, kind, mat)
+
+
+def load_camera_txt(path):
+    out = {}
+    for line in open(path):
+        t = line.split()
+        vals = [float(x) for x in t[1:]]
+        out[t[0]] = vals if len(vals) > 1 else vals[0]
+    return out

@@ -1,0 +1,230 @@
+"""a_dive_into_ray_tracing_amd — MI355X-native path tracer for the RTIOW final scene.
+
+Python view of librtmi.so (include/rtmi.h), used by the tests and bench.py.
+The product is the C ABI and its HIP kernels; this module only marshals
+arrays.  Names mirror the reference (rt_in_one_weekend/):
+
+    world = random_scene()                      # main.cpp:86-131
+    cam = camera(lookfrom, lookat, vup, vfov, aspect, aperture, focus)  # camera.h:8-45
+    sums = render(W, H, spp, max_depth, world, cam)   # worker() main.cpp:267-290
+    write_ppm("-", sums, spp)                   # write_color color.h:14-28
+
+There is no CPU fallback: render() raises RTError(RT_ENODEVICE) without a
+gfx950 GPU.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+from ._abi import RT_MAT_DIELECTRIC, RT_MAT_LAMBERTIAN, RT_MAT_METAL, RtCamera, RTError, RtScene, check, load
+
+__all__ = [
+    "RTError", "World", "lambertian", "metal", "dielectric", "sphere", "random_scene", "learn_scene",
+    "camera", "final_camera", "learn_camera", "Renderer", "render", "quantize", "write_ppm", "device_count",
+]
+
+_dp = C.POINTER(C.c_double)
+_fp = C.POINTER(C.c_float)
+_ip = C.POINTER(C.c_int32)
+
+
+def _d(a):
+    return a.ctypes.data_as(_dp)
+
+
+# ---------------------------------------------------------------- scene ----
+def lambertian(albedo):
+    """material.h:15-35"""
+    return (RT_MAT_LAMBERTIAN, (float(albedo[0]), float(albedo[1]), float(albedo[2]), 0.0))
+
+
+def metal(albedo, fuzz):
+    """material.h:37-54 (fuzz clamped to 1 as the constructor does, :39)"""
+    f = float(fuzz)
+    return (RT_MAT_METAL, (float(albedo[0]), float(albedo[1]), float(albedo[2]), f if f < 1 else 1.0))
+
+
+def dielectric(ir):
+    """material.h:56-97"""
+    return (RT_MAT_DIELECTRIC, (0.0, 0.0, 0.0, float(ir)))
+
+
+def sphere(center, radius, material):
+    """sphere.h:7-19"""
+    return (tuple(float(c) for c in center), float(radius), material)
+
+
+class World:
+    """hittable_list of spheres (hittable_list.h:6-18) as the flat arrays of rt_scene."""
+
+    def __init__(self, center_radius=None, mat_kind=None, mat_params=None):
+        self.center_radius = np.zeros((0, 4)) if center_radius is None else np.asarray(center_radius, np.float64).reshape(-1, 4)
+        self.mat_kind = np.zeros(0, np.int32) if mat_kind is None else np.asarray(mat_kind, np.int32).reshape(-1)
+        self.mat_params = np.zeros((0, 4)) if mat_params is None else np.asarray(mat_params, np.float64).reshape(-1, 4)
+
+    def add(self, obj):
+        (center, radius, (kind, params)) = obj
+        self.center_radius = np.vstack([self.center_radius, [*center, radius]])
+        self.mat_kind = np.append(self.mat_kind, np.int32(kind))
+        self.mat_params = np.vstack([self.mat_params, params])
+        return self
+
+    def __len__(self):
+        return int(self.mat_kind.size)
+
+    def c_struct(self):
+        self._keep = [np.ascontiguousarray(self.center_radius), np.ascontiguousarray(self.mat_kind), np.ascontiguousarray(self.mat_params)]
+        g, k, m = self._keep
+        return RtScene(len(self), _d(g), k.ctypes.data_as(_ip), _d(m))
+
+
+def random_scene(glibc_seed=1):
+    """random_scene() main.cpp:86-131 (487 spheres for the reference's seed 1)."""
+    L = load()
+    g, m = np.zeros(4 * 1024), np.zeros(4 * 1024)
+    k = np.zeros(1024, np.int32)
+    n = C.c_int32()
+    check(L.rt_scene_random(glibc_seed, _d(g), k.ctypes.data_as(_ip), _d(m), 1024, C.byref(n)), "rt_scene_random")
+    return World(g[: 4 * n.value], k[: n.value], m[: 4 * n.value])
+
+
+def learn_scene():
+    """learn() world main.cpp:198-210 (config 1)."""
+    L = load()
+    g, m = np.zeros(20), np.zeros(20)
+    k = np.zeros(5, np.int32)
+    n = C.c_int32()
+    check(L.rt_scene_learn(_d(g), k.ctypes.data_as(_ip), _d(m), 5, C.byref(n)), "rt_scene_learn")
+    return World(g, k, m)
+
+
+# --------------------------------------------------------------- camera ----
+def camera(lookfrom, lookat, vup, vfov, aspect_ratio, aperture, focus_dist):
+    """camera::camera camera.h:8-45 -> RtCamera (public fields camera.h:64-70)."""
+    cam = RtCamera()
+    a = [np.ascontiguousarray(x, dtype=np.float64) for x in (lookfrom, lookat, vup)]
+    check(load().rt_camera_init(C.byref(cam), _d(a[0]), _d(a[1]), _d(a[2]), vfov, aspect_ratio, aperture, focus_dist), "rt_camera_init")
+    return cam
+
+
+def final_camera(aspect_ratio=1.5):
+    """parallel_render() camera main.cpp:304-311"""
+    return camera((13, 2, 3), (0, 0, 0), (0, 1, 0), 20.0, aspect_ratio, 0.1, 10.0)
+
+
+def learn_camera(aspect_ratio=16.0 / 9.0):
+    """learn() camera main.cpp:212-221"""
+    lf, la = np.array([3.0, 3.0, 2.0]), np.array([0.0, 0.0, -1.0])
+    d = lf - la
+    return camera(lf, la, (0, 1, 0), 20.0, aspect_ratio, 0.5, float(np.sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2])))
+
+
+# ---------------------------------------------------------------- render ---
+def device_count():
+    n = C.c_int32(0)
+    rc = load().rt_device_count(C.byref(n))
+    return n.value if rc == 0 else 0
+
+
+class Renderer:
+    """One rt_ctx: a device, its stream and the resident scene."""
+
+    def __init__(self, world, device=0, tile_w=8, chunk=0):
+        self.L = load()
+        self._h = C.c_void_p()
+        check(self.L.rt_ctx_create(device, C.byref(self._h)), "rt_ctx_create")
+        self.device = device
+        self.set_scene(world)
+        self.set_tuning(tile_w, chunk)
+
+    def set_scene(self, world):
+        sc = world.c_struct()
+        check(self.L.rt_ctx_set_scene(self._h, C.byref(sc)), "rt_ctx_set_scene")
+
+    def set_tuning(self, tile_w=8, chunk=0):
+        check(self.L.rt_ctx_set_tuning(self._h, tile_w, chunk), "rt_ctx_set_tuning")
+
+    def render(self, cam, W, H, spp, max_depth=50, seed=1984):
+        """Whole image, host float32 sums [H, W, 3], row 0 = bottom (main.cpp:274)."""
+        out = np.zeros(W * H * 3, np.float32)
+        check(self.L.rt_render(self._h, C.byref(cam), W, H, spp, max_depth, seed, out.ctypes.data_as(_fp)), "rt_render")
+        return out.reshape(H, W, 3)
+
+    def render_rows(self, cam, W, H, spp, max_depth, seed, row0, row_step, nrows, dev_ptr, stream=0):
+        """Rows row0 + r*row_step into a device strip (async on `stream`)."""
+        check(
+            self.L.rt_render_rows(self._h, C.byref(cam), W, H, spp, max_depth, seed, row0, row_step, nrows, C.c_void_p(dev_ptr), C.c_void_p(stream)),
+            "rt_render_rows",
+        )
+
+    def last_segments(self):
+        """world.hit calls of the last render (GPU-counted)."""
+        v = C.c_uint64()
+        check(self.L.rt_ctx_last_segments(self._h, C.byref(v)), "rt_ctx_last_segments")
+        return v.value
+
+    def synchronize(self):
+        check(self.L.rt_ctx_synchronize(self._h), "rt_ctx_synchronize")
+
+    def replay_worker(self, cam, W, H, spp, max_depth, jobs, streams):
+        """Exact (double) replay of reference worker(start,end) calls with supplied rand() streams.
+        jobs: [(start, end), ...]; streams: list of int32 arrays (one per job)."""
+        ranges = np.ascontiguousarray(np.asarray(jobs, np.int32).reshape(-1))
+        offs = np.zeros(len(jobs) + 1, np.int64)
+        offs[1:] = np.cumsum([len(s) for s in streams])
+        flat = np.ascontiguousarray(np.concatenate([np.asarray(s, np.int32) for s in streams]) if offs[-1] else np.zeros(1, np.int32))
+        total = sum(3 * (e - s) for s, e in jobs)
+        out = np.zeros(max(total, 1))
+        used = np.zeros(len(jobs), np.int64)
+        check(
+            self.L.rt_replay_worker(
+                self._h, C.byref(cam), W, H, spp, max_depth, len(jobs), ranges.ctypes.data_as(_ip), flat.ctypes.data_as(_ip),
+                offs.ctypes.data_as(C.POINTER(C.c_int64)), _d(out), used.ctypes.data_as(C.POINTER(C.c_int64)),
+            ),
+            "rt_replay_worker",
+        )
+        return out[:total], used
+
+    def close(self):
+        if self._h:
+            self.L.rt_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def render(W, H, spp, max_depth, world, cam, seed=1984, device=0):
+    """The reference's render surface: image sums [H, W, 3] float32 (row 0 = bottom)."""
+    r = Renderer(world, device)
+    try:
+        return r.render(cam, W, H, spp, max_depth, seed)
+    finally:
+        r.close()
+
+
+def render_multi(W, H, spp, max_depth, world, cam, seed=1984, n_gpus=0):
+    """Single-process multi-GPU render (interleaved rows + one RCCL gather)."""
+    out = np.zeros(W * H * 3, np.float32)
+    sc = world.c_struct()
+    check(load().rt_render_multi(C.byref(sc), C.byref(cam), W, H, spp, max_depth, seed, n_gpus, out.ctypes.data_as(_fp)), "rt_render_multi")
+    return out.reshape(H, W, 3)
+
+
+def quantize(sums, spp):
+    """write_color quantisation color.h:14-28 -> uint8 [H, W, 3], top row first."""
+    s = np.ascontiguousarray(sums, np.float32)
+    H, W, _ = s.shape
+    rgb = np.zeros(W * H * 3, np.uint8)
+    check(load().rt_quantize(s.ctypes.data_as(_fp), W, H, spp, rgb.ctypes.data_as(C.POINTER(C.c_uint8))), "rt_quantize")
+    return rgb.reshape(H, W, 3)
+
+
+def write_ppm(path, sums, spp, binary=False):
+    s = np.ascontiguousarray(sums, np.float32)
+    H, W, _ = s.shape
+    check(load().rt_write_ppm(path.encode(), s.ctypes.data_as(_fp), W, H, spp, int(binary)), "rt_write_ppm")

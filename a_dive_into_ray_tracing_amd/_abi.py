@@ -1,0 +1,94 @@
+"""ctypes declarations for librtmi.so (include/rtmi.h).
+
+The library is built in-tree by `make -C a_dive_into_ray_tracing_amd/csrc`
+(or `__graft_entry__.build()`) into a_dive_into_ray_tracing_amd/lib/.  There is
+no fallback: if the library is missing, importing the bindings raises.
+"""
+import ctypes as C
+import os
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "librtmi.so")
+
+RT_OK = 0
+ERRORS = {
+    -1: "RT_EINVAL",
+    -2: "RT_EHIP",
+    -3: "RT_ENODEVICE",
+    -4: "RT_EUNSUPPORTED",
+    -5: "RT_ENOMEM",
+    -6: "RT_ERCCL",
+    -7: "RT_EIO",
+    -8: "RT_ESTREAM",
+}
+RT_MAT_LAMBERTIAN, RT_MAT_METAL, RT_MAT_DIELECTRIC = 0, 1, 2
+
+_dp = C.POINTER(C.c_double)
+_fp = C.POINTER(C.c_float)
+_ip = C.POINTER(C.c_int32)
+_lp = C.POINTER(C.c_int64)
+
+
+class RtScene(C.Structure):
+    _fields_ = [("n", C.c_int32), ("center_radius", _dp), ("mat_kind", _ip), ("mat_params", _dp)]
+
+
+class RtCamera(C.Structure):
+    _fields_ = [(nm, C.c_double * 3) for nm in ("origin", "lower_left_corner", "horizontal", "vertical", "u", "v", "w")] + [
+        ("lens_radius", C.c_double)
+    ]
+
+
+class RTError(RuntimeError):
+    def __init__(self, what, code, msg):
+        super().__init__(f"{what} failed: {ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+# every symbol include/rtmi.h declares: name -> (restype, argtypes)
+SIGNATURES = {
+    "rt_last_error": (C.c_char_p, []),
+    "rt_version": (C.c_int, []),
+    "rt_camera_init": (C.c_int, [C.POINTER(RtCamera), _dp, _dp, _dp, C.c_double, C.c_double, C.c_double, C.c_double]),
+    "rt_scene_random": (C.c_int, [C.c_uint32, _dp, _ip, _dp, C.c_int32, _ip]),
+    "rt_scene_learn": (C.c_int, [_dp, _ip, _dp, C.c_int32, _ip]),
+    "rt_write_ppm": (C.c_int, [C.c_char_p, _fp, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "rt_quantize": (C.c_int, [_fp, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]),
+    "rt_device_count": (C.c_int, [_ip]),
+    "rt_ctx_create": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
+    "rt_ctx_destroy": (C.c_int, [C.c_void_p]),
+    "rt_ctx_set_scene": (C.c_int, [C.c_void_p, C.POINTER(RtScene)]),
+    "rt_ctx_set_tuning": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    "rt_render": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_uint64, _fp]),
+    "rt_render_rows": (
+        C.c_int,
+        [C.c_void_p, C.POINTER(RtCamera)] + [C.c_int32] * 4 + [C.c_uint64] + [C.c_int32] * 3 + [C.c_void_p, C.c_void_p],
+    ),
+    "rt_ctx_synchronize": (C.c_int, [C.c_void_p]),
+    "rt_ctx_last_segments": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    "rt_replay_worker": (C.c_int, [C.c_void_p, C.POINTER(RtCamera)] + [C.c_int32] * 5 + [_ip, _ip, _lp, _dp, _lp]),
+    "rt_render_multi": (C.c_int, [C.POINTER(RtScene), C.POINTER(RtCamera)] + [C.c_int32] * 4 + [C.c_uint64, C.c_int32, _fp]),
+}
+
+_lib = None
+
+
+def load():
+    """Load librtmi.so once; raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"librtmi.so not built at {LIB_PATH}: run `make -C a_dive_into_ray_tracing_amd/csrc`")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, what):
+    if rc != RT_OK:
+        raise RTError(what, rc, load().rt_last_error().decode(errors="replace"))
+    return rc

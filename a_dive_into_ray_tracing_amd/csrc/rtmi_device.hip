@@ -1,0 +1,843 @@
+// rtmi_device.hip — device half of librtmi.so: the gfx950 path-tracing
+// kernels and the C-ABI entry points that launch them.
+//
+// Hot path: the per-pixel sample loop of the
+// reference — camera ray (camera.h:56-62), the iterative ray_color bounce
+// loop (main.cpp:57-83), hittable_list::hit / sphere::hit (hittable_list.h:
+// 20-34, sphere.h:21-55), lambertian/metal/dielectric scatter (material.h),
+// RNG (rtweekend.h:21-29) and the per-pixel sum (main.cpp:276-285).
+//
+// MI355X design:
+//  * One wavefront owns a work item = (64-pixel tile, range of samples).
+//    Lanes take (pixel, sample) jobs from a wave-local queue: when a lane's
+//    path terminates, __ballot + mbcnt hand it the next job (path
+//    regeneration with wavefront prefix compaction), so lanes stay busy until
+//    the item's last samples and never wait for the slowest pixel.
+//  * The sphere loop is wave-uniform: sphere k's {centre, r^2} is one
+//    s_load_dwordx4 into SGPRs for the whole wave (scalar cache, 16 B per
+//    sphere), so the VALU does only the ray-sphere arithmetic.
+//  * Counter-based RNG (xoroshiro128+ seeded per (seed, pixel, sample)) and
+//    int64 fixed-point accumulation (LDS ds_add_u64, then one global atomic
+//    per pixel per item) make the image independent of scheduling, tiling,
+//    partition and GPU count, and bit-identical to the CPU restatement
+//    (oracle/, fast mode).
+//  * No MFMA: this is branchy scalar FP32 (VALU roofline).
+//
+// Numerics: compiled with -ffp-contract=off; every FMA is an explicit
+// __builtin_fma(f); division and sqrt are IEEE correctly rounded (hipcc
+// default).  The DOUBLE instantiation (FAST=false) reproduces the reference
+// bit-for-bit given its rand() stream (rt_replay_worker).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "rtmi_internal.h"
+
+namespace rtmi {
+
+// ---------------------------------------------------------------------------
+// numeric policy
+// ---------------------------------------------------------------------------
+template <class R> struct V3 { R x, y, z; };
+template <class R> __host__ __device__ __forceinline__ V3<R> mk(R x, R y, R z) { return V3<R>{x, y, z}; }
+
+template <bool F> __device__ __forceinline__ float madd(float a, float b, float c) {
+  if constexpr (F) return __builtin_fmaf(a, b, c);
+  else return a * b + c;
+}
+template <bool F> __device__ __forceinline__ double madd(double a, double b, double c) {
+  if constexpr (F) return __builtin_fma(a, b, c);
+  else return a * b + c;
+}
+__device__ __forceinline__ float dsqrt(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ double dsqrt(double x) { return __builtin_sqrt(x); }
+__device__ __forceinline__ float dfabs(float x) { return __builtin_fabsf(x); }
+__device__ __forceinline__ double dfabs(double x) { return __builtin_fabs(x); }
+__device__ __forceinline__ float dfmin(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ double dfmin(double a, double b) { return __builtin_fmin(a, b); }
+// pow((1-cosine), 5) material.h:95: the exact path uses the library pow; the
+// fast path multiplies (x^2)^2 * x (the CPU restatement does the same).
+__device__ __forceinline__ float pow5(float x) { float x2 = x * x; float x4 = x2 * x2; return x4 * x; }
+__device__ __forceinline__ double pow5(double x) { return pow(x, 5.0); }
+
+// dot vec3.h:77-79
+template <bool F, class R> __device__ __forceinline__ R dot(V3<R> a, V3<R> b) {
+  return madd<F>(a.z, b.z, madd<F>(a.y, b.y, a.x * b.x));
+}
+template <class R> __device__ __forceinline__ V3<R> scale(R t, V3<R> v) { return mk(t * v.x, t * v.y, t * v.z); }
+// unit_vector vec3.h:101 (operator/ is (1/t)*v, vec3.h:89)
+template <bool F, class R> __device__ __forceinline__ V3<R> unit(V3<R> v) {
+  return scale(R(1) / dsqrt(dot<F>(v, v)), v);
+}
+// reflect vec3.h:114
+template <bool F, class R> __device__ __forceinline__ V3<R> reflect(V3<R> v, V3<R> n) {
+  const R k = R(2) * dot<F>(v, n);
+  return mk(madd<F>(-k, n.x, v.x), madd<F>(-k, n.y, v.y), madd<F>(-k, n.z, v.z));
+}
+// refract vec3.h:116-121 (cos_theta identical to the caller's, material.h:72)
+template <bool F, class R> __device__ __forceinline__ V3<R> refract(V3<R> uv, V3<R> n, R eta, R cos_theta) {
+  V3<R> perp = mk(eta * madd<F>(cos_theta, n.x, uv.x), eta * madd<F>(cos_theta, n.y, uv.y),
+                  eta * madd<F>(cos_theta, n.z, uv.z));
+  const R s = dsqrt(dfabs(R(1) - dot<F>(perp, perp)));
+  return mk(madd<F>(-s, n.x, perp.x), madd<F>(-s, n.y, perp.y), madd<F>(-s, n.z, perp.z));
+}
+// dielectric::reflectance material.h:91-96 (Schlick)
+template <bool F, class R> __device__ __forceinline__ R reflectance(R cosine, R ref_idx) {
+  R r0 = (R(1) - ref_idx) / (R(1) + ref_idx);
+  r0 = r0 * r0;
+  return madd<F>(R(1) - r0, pow5(R(1) - cosine), r0);
+}
+// near_zero vec3.h:53-57 — keeps the reference's fabs(e[0] < s) slip
+template <class R> __device__ __forceinline__ bool near_zero(V3<R> v) {
+  const R s = R(1e-8);
+  return (v.x < s) && (dfabs(v.y) < s) && (dfabs(v.z) < s);
+}
+
+// ---------------------------------------------------------------------------
+// RNG
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+// xoroshiro128+ (a=24, b=16, c=37), state from splitmix64 finalisers of the
+// key (seed, pixel, sample): a counter-based stream per camera sample.
+struct Xoro {
+  uint64_t s0, s1;
+  __device__ __forceinline__ void init(uint64_t seed, uint64_t pixel, uint32_t sample) {
+    const uint64_t key = (pixel << 24) | uint64_t(sample);
+    s0 = mix64(seed ^ mix64(key + 0x9E3779B97F4A7C15ULL));
+    s1 = mix64(s0 + 0x9E3779B97F4A7C15ULL);
+  }
+  __device__ __forceinline__ uint64_t next() {
+    const uint64_t a = s0, r = s0 + s1;
+    uint64_t b = s1 ^ a;
+    s0 = ((a << 24) | (a >> 40)) ^ b ^ (b << 16);
+    s1 = (b << 37) | (b >> 27);
+    return r;
+  }
+  // top 24 bits: uniform on [0,1) exactly representable in float
+  __device__ __forceinline__ float uni() { return float(uint32_t(next() >> 40)) * 0x1p-24f; }
+};
+
+// Replays a supplied glibc rand() stream: random_double() = rand()/(RAND_MAX+1.0)
+struct StreamRng {
+  const int32_t *p;
+  int64_t pos, end;
+  bool overflow;
+  __device__ __forceinline__ double uni() {
+    if (pos < end) return double(p[pos++]) / 2147483648.0;
+    overflow = true;
+    return 0.5;
+  }
+};
+
+// random_double(-1,1) rtweekend.h:26-29: min + (max-min)*rd()
+template <class R, class G> __device__ __forceinline__ R rd_m11(G &g) { return R(-1) + R(2) * R(g.uni()); }
+// random_in_unit_sphere vec3.h:103-110: vec3::random(-1,1) draws z, y, x (GCC)
+template <bool F, class R, class G> __device__ __forceinline__ V3<R> in_sphere(G &g) {
+  for (;;) {
+    const R z = rd_m11<R>(g);
+    const R y = rd_m11<R>(g);
+    const R x = rd_m11<R>(g);
+    const V3<R> p = mk(x, y, z);
+    if (dot<F>(p, p) >= R(1)) continue;
+    return p;
+  }
+}
+// random_in_unit_disk vec3.h:123-130: draws y, x (GCC)
+template <bool F, class R, class G> __device__ __forceinline__ V3<R> in_disk(G &g) {
+  for (;;) {
+    const R y = rd_m11<R>(g);
+    const R x = rd_m11<R>(g);
+    if (madd<F>(y, y, x * x) >= R(1)) continue;
+    return mk(x, y, R(0));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// scene / camera views
+// ---------------------------------------------------------------------------
+template <class R> struct V4T;
+template <> struct V4T<float> { using type = float4; };
+template <> struct V4T<double> { using type = double4; };
+
+// geom[k]  = {cx, cy, cz, r*r}
+// shade0[k] = {1/r, albedo r, g, b}
+// shade1[k] = {kind, fuzz (clamped), ir, 1/ir}
+template <class R> struct SceneView {
+  const typename V4T<R>::type *__restrict__ geom;
+  const typename V4T<R>::type *__restrict__ sh0;
+  const typename V4T<R>::type *__restrict__ sh1;
+  int32_t n;
+};
+
+template <class R> struct Cam {
+  V3<R> origin, llc, hor, ver, u, v;
+  R lens;
+};
+
+// camera::get_ray camera.h:56-62
+template <bool F, class R, class G>
+__device__ __forceinline__ void get_ray(const Cam<R> &c, R s, R t, G &g, V3<R> &o, V3<R> &d) {
+  const V3<R> p = in_disk<F, R>(g);
+  const R rdx = c.lens * p.x, rdy = c.lens * p.y;
+  const V3<R> off = mk(madd<F>(rdy, c.v.x, rdx * c.u.x), madd<F>(rdy, c.v.y, rdx * c.u.y),
+                       madd<F>(rdy, c.v.z, rdx * c.u.z));
+  o = mk(c.origin.x + off.x, c.origin.y + off.y, c.origin.z + off.z);
+  d = mk((madd<F>(t, c.ver.x, madd<F>(s, c.hor.x, c.llc.x)) - c.origin.x) - off.x,
+         (madd<F>(t, c.ver.y, madd<F>(s, c.hor.y, c.llc.y)) - c.origin.y) - off.y,
+         (madd<F>(t, c.ver.z, madd<F>(s, c.hor.z, c.llc.z)) - c.origin.z) - off.z);
+}
+
+// hittable_list::hit over sphere::hit: closest root in the closed interval
+// [t_min, closest_so_far]; ties go to the later object (sphere.h:36-41).
+// The (hb >= 0 && cc >= 0) skip never changes the result: both roots are
+// <= 0 < t_min there.  In the fast path the wave runs this
+// loop in lockstep with sphere k in SGPRs.
+template <bool F, class R>
+__device__ __forceinline__ int32_t hit_world(const SceneView<R> &sc, V3<R> o, V3<R> d, R &t_hit) {
+  const R a = dot<F>(d, d);
+  const R inv_a = R(1) / a;
+  const R t_min = R(0.001);
+  R t_max = R(INFINITY);
+  int32_t best = -1;
+#pragma unroll 4
+  for (int32_t k = 0; k < sc.n; ++k) {
+    const auto s = sc.geom[k];
+    const R ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;
+    const R hb = madd<F>(ocz, d.z, madd<F>(ocy, d.y, ocx * d.x));
+    const R cc = madd<F>(ocz, ocz, madd<F>(ocy, ocy, ocx * ocx)) - s.w;
+    const R disc = madd<F>(hb, hb, -(a * cc));
+    if (!(disc < R(0)) && !(hb >= R(0) && cc >= R(0))) {
+      const R sq = dsqrt(disc);
+      R root = F ? (-hb - sq) * inv_a : (-hb - sq) / a;
+      bool ok = !(root < t_min || t_max < root);
+      if (!ok) {
+        root = F ? (-hb + sq) * inv_a : (-hb + sq) / a;
+        ok = !(root < t_min || t_max < root);
+      }
+      if (ok) {
+        t_max = root;
+        best = k;
+      }
+    }
+  }
+  t_hit = t_max;
+  return best;
+}
+
+// material::scatter material.h:15-97.  Returns true if the ray scattered.
+template <bool F, class R, class G>
+__device__ __forceinline__ bool scatter(const SceneView<R> &sc, int32_t k, V3<R> din, V3<R> normal,
+                                        bool front, G &g, V3<R> &atten, V3<R> &dout) {
+  const auto s0 = sc.sh0[k];
+  const auto s1 = sc.sh1[k];
+  const int kind = int(s1.x);
+  if (kind == RT_MAT_LAMBERTIAN) {  // material.h:19-31
+    const V3<R> ru = unit<F>(in_sphere<F, R>(g));
+    V3<R> dir = mk(normal.x + ru.x, normal.y + ru.y, normal.z + ru.z);
+    if (near_zero(dir)) dir = normal;
+    dout = dir;
+    atten = mk(s0.y, s0.z, s0.w);
+    return true;
+  }
+  if (kind == RT_MAT_METAL) {  // material.h:40-49
+    const V3<R> refl = reflect<F>(unit<F>(din), normal);
+    const V3<R> rv = in_sphere<F, R>(g);
+    const R fz = s1.y;
+    const V3<R> dir = mk(madd<F>(fz, rv.x, refl.x), madd<F>(fz, rv.y, refl.y), madd<F>(fz, rv.z, refl.z));
+    dout = dir;
+    atten = mk(s0.y, s0.z, s0.w);
+    return dot<F>(dir, normal) > R(0);
+  }
+  // dielectric material.h:60-85
+  atten = mk(R(1), R(1), R(1));
+  const R ratio = front ? s1.w : s1.z;
+  const V3<R> ud = unit<F>(din);
+  const R cos_theta = dfmin(dot<F>(mk(-ud.x, -ud.y, -ud.z), normal), R(1));
+  const R sin_theta = dsqrt(madd<F>(-cos_theta, cos_theta, R(1)));
+  const bool cannot_refract = ratio * sin_theta > R(1);
+  if (cannot_refract || reflectance<F>(cos_theta, ratio) > R(g.uni()))
+    dout = reflect<F>(ud, normal);
+  else
+    dout = refract<F>(ud, normal, ratio, cos_theta);
+  return true;
+}
+
+// Hit record (sphere.h:43-53, hittable.h:23-26) for sphere k at t.
+template <bool F, class R>
+__device__ __forceinline__ void hit_record(const SceneView<R> &sc, int32_t k, V3<R> o, V3<R> d, R t,
+                                           V3<R> &p, V3<R> &normal, bool &front) {
+  const auto g = sc.geom[k];
+  const R inv_r = sc.sh0[k].x;
+  p = mk(madd<F>(t, d.x, o.x), madd<F>(t, d.y, o.y), madd<F>(t, d.z, o.z));  // ray::at ray.h:15
+  const V3<R> outward = scale(inv_r, mk(p.x - g.x, p.y - g.y, p.z - g.z));
+  front = dot<F>(d, outward) < R(0);
+  normal = front ? outward : mk(-outward.x, -outward.y, -outward.z);
+}
+
+// sky, main.cpp:80-82
+template <bool F, class R> __device__ __forceinline__ V3<R> sky(V3<R> d) {
+  const R uy = (R(1) / dsqrt(dot<F>(d, d))) * d.y;
+  const R t = R(0.5) * (uy + R(1));
+  return mk(madd<F>(t, R(0.5), R(1) - t), madd<F>(t, R(0.7), R(1) - t), madd<F>(t, R(1), R(1) - t));
+}
+
+// ---------------------------------------------------------------------------
+// fast render kernel
+// ---------------------------------------------------------------------------
+struct RenderArgs {
+  Cam<float> cam;
+  int32_t n, W, H, spp, max_depth;
+  uint64_t seed;
+  int32_t row0, row_step, nrows_valid;
+  int32_t tiles_x, chunk, n_chunks, n_items;
+};
+
+constexpr int kWavesPerBlock = 4;
+
+__device__ __forceinline__ int64_t to_fixed(float c) { return int64_t(c * 4294967296.0f); }
+__device__ __forceinline__ float from_fixed(int64_t v) { return float(v) * 0x1p-32f; }
+
+template <int TW, bool CHUNKED>
+__global__ __launch_bounds__(64 * kWavesPerBlock) void render_kernel(
+    const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1,
+    RenderArgs a, unsigned long long *__restrict__ accum, float *__restrict__ out,
+    unsigned long long *__restrict__ segments) {
+  constexpr int TH = 64 / TW;
+  __shared__ unsigned long long acc[kWavesPerBlock][3][64];
+  __shared__ unsigned long long wave_segs[kWavesPerBlock];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int item = blockIdx.x * kWavesPerBlock + wave;
+  if (item >= a.n_items) return;  // wave-uniform; no block barrier follows
+
+  const int tile = item / a.n_chunks;
+  const int chunk = item - tile * a.n_chunks;
+  const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
+  const int x0 = tx * TW, y0 = ty * TH;
+  const int vw = min(TW, a.W - x0), vh = min(TH, a.nrows_valid - y0);
+  const int nv = vw * vh;  // valid pixels of this tile
+  const int s0 = chunk * a.chunk;
+  const int ns = min(a.chunk, a.spp - s0);
+  const int nq = nv * ns;  // jobs: (pixel, sample) pairs of this item
+
+  acc[wave][0][lane] = 0;
+  acc[wave][1][lane] = 0;
+  acc[wave][2][lane] = 0;
+  if (lane == 0) wave_segs[wave] = 0;
+  unsigned nseg = 0;  // world.hit calls of this lane (algorithmic-work accounting)
+
+  const SceneView<float> sc{geom, sh0, sh1, a.n};
+  const float inv_wm1 = 0.f;  // (unused; divisions below follow main.cpp:278-279)
+  (void)inv_wm1;
+
+  V3<float> o, d, T;
+  int px = 0, depth = 0;
+  Xoro rng;
+
+  // job q -> pixel px = q % nv, sample s0 + q / nv (sample-major, so every
+  // pixel of the tile advances together); then the camera ray.
+  auto start = [&](int q) {
+    const int s = s0 + q / nv;
+    px = q - (q / nv) * nv;
+    const int ly = px / vw, lx = px - ly * vw;
+    const int i = x0 + lx;
+    const int j = a.row0 + (y0 + ly) * a.row_step;
+    rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(s));
+    const float u = (float(i) + rng.uni()) / float(a.W - 1);  // main.cpp:278
+    const float v = (float(j) + rng.uni()) / float(a.H - 1);  // main.cpp:279
+    get_ray<true, float>(a.cam, u, v, rng, o, d);
+    T = mk(1.f, 1.f, 1.f);
+    depth = 0;
+  };
+
+  bool active = lane < nq;
+  if (active) start(lane);
+  int next = 64;
+
+  for (;;) {
+    if (__ballot(active) == 0) break;
+    bool done = false;
+    V3<float> col = mk(0.f, 0.f, 0.f);
+    if (active) {
+      float t;
+      ++nseg;
+      const int k = hit_world<true, float>(sc, o, d, t);
+      if (k < 0) {
+        const V3<float> sk = sky<true, float>(d);
+        col = mk(T.x * sk.x, T.y * sk.y, T.z * sk.z);
+        done = true;
+      } else {
+        V3<float> p, nrm, at, nd;
+        bool front;
+        hit_record<true, float>(sc, k, o, d, t, p, nrm, front);
+        if (!scatter<true, float>(sc, k, d, nrm, front, rng, at, nd)) {
+          done = true;  // absorbed (metal below the surface): black, main.cpp:78
+        } else {
+          T = mk(T.x * at.x, T.y * at.y, T.z * at.z);
+          o = p;
+          d = nd;
+          if (++depth >= a.max_depth) done = true;  // depth exhausted: black, main.cpp:58-60
+        }
+      }
+    }
+    const unsigned long long m = __ballot(done);
+    if (m) {
+      if (done) {
+        atomicAdd(&acc[wave][0][px], (unsigned long long)to_fixed(col.x));
+        atomicAdd(&acc[wave][1][px], (unsigned long long)to_fixed(col.y));
+        atomicAdd(&acc[wave][2][px], (unsigned long long)to_fixed(col.z));
+        const int rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
+        const int q = next + rank;
+        if (q < nq) start(q);
+        else active = false;
+      }
+      next += __popcll(m);
+    }
+  }
+
+  atomicAdd(&wave_segs[wave], (unsigned long long)nseg);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) atomicAdd(segments, wave_segs[wave]);
+  if (lane < nv) {
+    const int ly = lane / vw, lx = lane - ly * vw;
+    const size_t o3 = (size_t(y0 + ly) * size_t(a.W) + size_t(x0 + lx)) * 3;
+    for (int c = 0; c < 3; ++c) {
+      const unsigned long long v = acc[wave][c][lane];
+      if constexpr (CHUNKED) atomicAdd(&accum[o3 + c], v);
+      else out[o3 + c] = from_fixed((long long)v);
+    }
+  }
+}
+
+__global__ void finalize_kernel(const unsigned long long *__restrict__ accum, float *__restrict__ out, size_t n) {
+  const size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = from_fixed((long long)accum[i]);
+}
+
+// ---------------------------------------------------------------------------
+// exact replay kernel (double, reference op order, supplied rand() stream)
+// ---------------------------------------------------------------------------
+constexpr int kMaxReplayDepth = 64;
+
+struct ReplayArgs {
+  Cam<double> cam;
+  int32_t n, W, H, spp, max_depth, n_jobs;
+};
+
+// ray_color main.cpp:57-83 with the recursion's product order: the colour is
+// attenuation_1 * (attenuation_2 * (... * sky)), combined innermost first.
+__device__ V3<double> ray_color_exact(const SceneView<double> &sc, V3<double> o, V3<double> d, int max_depth,
+                                      StreamRng &g) {
+  V3<double> att[kMaxReplayDepth];
+  int n_att = 0;
+  V3<double> col = mk(0.0, 0.0, 0.0);
+  for (int depth = max_depth; depth > 0; depth--) {
+    double t;
+    const int k = hit_world<false, double>(sc, o, d, t);
+    if (k < 0) {
+      col = sky<false, double>(d);
+      break;
+    }
+    V3<double> p, nrm, at, nd;
+    bool front;
+    hit_record<false, double>(sc, k, o, d, t, p, nrm, front);
+    if (!scatter<false, double>(sc, k, d, nrm, front, g, at, nd)) break;
+    att[n_att++] = at;
+    o = p;
+    d = nd;
+  }
+  for (int q = n_att - 1; q >= 0; q--) col = mk(att[q].x * col.x, att[q].y * col.y, att[q].z * col.z);
+  return col;
+}
+
+__global__ void replay_kernel(const double4 *__restrict__ geom, const double4 *__restrict__ sh0,
+                              const double4 *__restrict__ sh1, ReplayArgs a, const int32_t *__restrict__ ranges,
+                              const int32_t *__restrict__ streams, const int64_t *__restrict__ offs,
+                              const int64_t *__restrict__ out_offs, double *__restrict__ out,
+                              int64_t *__restrict__ used) {
+  const int job = blockIdx.x * blockDim.x + threadIdx.x;
+  if (job >= a.n_jobs) return;
+  const SceneView<double> sc{geom, sh0, sh1, a.n};
+  StreamRng g{streams, offs[job], offs[job + 1], false};
+  const int start = ranges[2 * job], end = ranges[2 * job + 1];
+  double *o = out + out_offs[job];
+  for (int index = start; index < end; index++) {  // worker() main.cpp:273-289
+    const int j = index / a.W, i = index % a.W;
+    V3<double> sum = mk(0.0, 0.0, 0.0);
+    for (int s = 0; s < a.spp; s++) {
+      const double u = (i + g.uni()) / (a.W - 1);
+      const double v = (j + g.uni()) / (a.H - 1);
+      V3<double> ro, rd;
+      get_ray<false, double>(a.cam, u, v, g, ro, rd);
+      const V3<double> c = ray_color_exact(sc, ro, rd, a.max_depth, g);
+      sum = mk(sum.x + c.x, sum.y + c.y, sum.z + c.z);
+    }
+    o[3 * (index - start) + 0] = sum.x;
+    o[3 * (index - start) + 1] = sum.y;
+    o[3 * (index - start) + 2] = sum.z;
+  }
+  used[job] = g.overflow ? -1 : g.pos - offs[job];
+}
+
+}  // namespace rtmi
+
+// ===========================================================================
+// host side
+// ===========================================================================
+using namespace rtmi;
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) return set_error(RT_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+struct rt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int32_t n = 0;
+  float4 *geom = nullptr, *sh0 = nullptr, *sh1 = nullptr;
+  double4 *geom64 = nullptr, *sh064 = nullptr, *sh164 = nullptr;
+  unsigned long long *accum = nullptr;
+  size_t accum_cap = 0;  // elements
+  float *scratch = nullptr;
+  size_t scratch_cap = 0;  // elements
+  unsigned long long *segments = nullptr;  // world.hit calls of the last render
+  hipStream_t last_stream = nullptr;
+  int32_t tile_w = 8;
+  int32_t chunk = 0;
+};
+
+namespace rtmi {
+hipStream_t ctx_stream(rt_ctx *ctx) { return ctx->stream; }
+}  // namespace rtmi
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+Cam<float> cam_f(const rt_camera *c) {
+  auto v = [](const double *p) { return mk(float(p[0]), float(p[1]), float(p[2])); };
+  return Cam<float>{v(c->origin), v(c->lower_left_corner), v(c->horizontal), v(c->vertical), v(c->u), v(c->v),
+                    float(c->lens_radius)};
+}
+Cam<double> cam_d(const rt_camera *c) {
+  auto v = [](const double *p) { return mk(p[0], p[1], p[2]); };
+  return Cam<double>{v(c->origin), v(c->lower_left_corner), v(c->horizontal), v(c->vertical), v(c->u), v(c->v),
+                     c->lens_radius};
+}
+
+template <class T> int dev_alloc(T **p, size_t count) {
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc(reinterpret_cast<void **>(p), count * sizeof(T));
+  if (e != hipSuccess) return set_error(RT_ENOMEM, "hipMalloc(%zu B): %s", count * sizeof(T), hipGetErrorString(e));
+  return RT_OK;
+}
+
+int check_render_args(const rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t spp, int32_t max_depth) {
+  if (!ctx || !cam) return set_error(RT_EINVAL, "null context or camera");
+  if (W < 2 || H < 2) return set_error(RT_EINVAL, "image must be at least 2x2 (u,v divide by W-1, H-1)");
+  if (spp < 1 || spp >= (1 << 24)) return set_error(RT_EINVAL, "spp must be in [1, 2^24)");
+  if (max_depth < 0) return set_error(RT_EINVAL, "max_depth must be >= 0");
+  if (int64_t(W) * int64_t(H) >= (int64_t(1) << 40)) return set_error(RT_EINVAL, "image too large");
+  if (ctx->n <= 0) return set_error(RT_EINVAL, "no scene uploaded (rt_ctx_set_scene)");
+  return RT_OK;
+}
+
+}  // namespace
+
+RTMI_EXPORT int rt_device_count(int32_t *n) {
+  if (!n) return set_error(RT_EINVAL, "null");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *n = 0;
+    return set_error(RT_ENODEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e));
+  }
+  *n = c;
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_ctx_create(int32_t device, rt_ctx **out) {
+  if (!out) return set_error(RT_EINVAL, "null out");
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return set_error(RT_ENODEVICE, "no HIP device visible");
+  if (device < 0 || device >= count) return set_error(RT_ENODEVICE, "device %d out of range [0,%d)", device, count);
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return set_error(RT_ENODEVICE, "device %d is %s; librtmi is built for gfx950 only", device, prop.gcnArchName);
+  DeviceGuard guard(device);
+  auto ctx = std::make_unique<rt_ctx>();
+  ctx->device = device;
+  HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+  if (int rc = dev_alloc(&ctx->segments, 1)) return rc;
+  HIP_TRY(hipMemset(ctx->segments, 0, sizeof(unsigned long long)));
+  *out = ctx.release();
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_ctx_destroy(rt_ctx *ctx) {
+  if (!ctx) return RT_OK;
+  DeviceGuard guard(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (void *p : {(void *)ctx->geom, (void *)ctx->sh0, (void *)ctx->sh1, (void *)ctx->geom64, (void *)ctx->sh064,
+                  (void *)ctx->sh164, (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments})
+    if (p) (void)hipFree(p);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
+  if (!ctx || !scene || scene->n <= 0 || !scene->center_radius || !scene->mat_kind || !scene->mat_params)
+    return set_error(RT_EINVAL, "rt_ctx_set_scene: bad argument");
+  const int n = scene->n;
+  std::vector<float4> g(n), s0(n), s1(n);
+  std::vector<double4> g64(n), s064(n), s164(n);
+  for (int k = 0; k < n; k++) {
+    const double *c = scene->center_radius + 4 * k;
+    const double *m = scene->mat_params + 4 * k;
+    const int kind = scene->mat_kind[k];
+    if (kind < RT_MAT_LAMBERTIAN || kind > RT_MAT_DIELECTRIC)
+      return set_error(RT_EUNSUPPORTED, "object %d: unsupported material kind %d", k, kind);
+    const double fuzz = m[3] < 1 ? m[3] : 1;  // metal ctor material.h:39
+    const float r = float(c[3]), ir = float(m[3]);
+    g[k] = make_float4(float(c[0]), float(c[1]), float(c[2]), r * r);
+    s0[k] = make_float4(1.0f / r, float(m[0]), float(m[1]), float(m[2]));
+    s1[k] = make_float4(float(kind), float(fuzz), ir, 1.0f / ir);
+    g64[k] = make_double4(c[0], c[1], c[2], c[3] * c[3]);
+    s064[k] = make_double4(1 / c[3], m[0], m[1], m[2]);
+    s164[k] = make_double4(double(kind), fuzz, m[3], 1.0 / m[3]);
+  }
+  DeviceGuard guard(ctx->device);
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  int rc;
+  if ((rc = dev_alloc(&ctx->geom, n)) || (rc = dev_alloc(&ctx->sh0, n)) || (rc = dev_alloc(&ctx->sh1, n)) ||
+      (rc = dev_alloc(&ctx->geom64, n)) || (rc = dev_alloc(&ctx->sh064, n)) || (rc = dev_alloc(&ctx->sh164, n)))
+    return rc;
+  HIP_TRY(hipMemcpy(ctx->geom, g.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(ctx->sh0, s0.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(ctx->sh1, s1.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(ctx->geom64, g64.data(), n * sizeof(double4), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(ctx->sh064, s064.data(), n * sizeof(double4), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(ctx->sh164, s164.data(), n * sizeof(double4), hipMemcpyHostToDevice));
+  ctx->n = n;
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_ctx_set_tuning(rt_ctx *ctx, int32_t tile_w, int32_t chunk) {
+  if (!ctx) return set_error(RT_EINVAL, "null ctx");
+  if (tile_w != 8 && tile_w != 16 && tile_w != 32 && tile_w != 64)
+    return set_error(RT_EINVAL, "tile_w must be 8, 16, 32 or 64");
+  if (chunk < 0) return set_error(RT_EINVAL, "chunk must be >= 0");
+  ctx->tile_w = tile_w;
+  ctx->chunk = chunk;
+  return RT_OK;
+}
+
+namespace {
+
+template <int TW>
+void launch_tw(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a,
+               unsigned long long *accum, float *out) {
+  if (chunked)
+    hipLaunchKernelGGL((render_kernel<TW, true>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
+                       ctx->sh1, a, accum, out, ctx->segments);
+  else
+    hipLaunchKernelGGL((render_kernel<TW, false>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
+                       ctx->sh1, a, accum, out, ctx->segments);
+}
+
+// The render of one row set into a device strip; all work on `st`.
+int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t spp, int32_t max_depth,
+                     uint64_t seed, int32_t row0, int32_t row_step, int32_t nrows, float *strip, hipStream_t st) {
+  const size_t n_out = size_t(nrows) * size_t(W) * 3;
+  ctx->last_stream = st;
+  HIP_TRY(hipMemsetAsync(ctx->segments, 0, sizeof(unsigned long long), st));
+  if (nrows == 0) return RT_OK;
+  // valid rows: row0 + r*row_step < H
+  int32_t nvalid = 0;
+  if (row0 < H) nvalid = std::min<int64_t>(nrows, (int64_t(H) - row0 + row_step - 1) / row_step);
+  if (nvalid < nrows)
+    HIP_TRY(hipMemsetAsync(strip + size_t(nvalid) * W * 3, 0, size_t(nrows - nvalid) * W * 3 * sizeof(float), st));
+  if (nvalid == 0) return RT_OK;
+  if (max_depth == 0) {  // ray_color returns black before any hit test (main.cpp:58-60)
+    HIP_TRY(hipMemsetAsync(strip, 0, size_t(nvalid) * W * 3 * sizeof(float), st));
+    return RT_OK;
+  }
+  const int TW = ctx->tile_w, TH = 64 / TW;
+  const int tiles_x = (W + TW - 1) / TW;
+  const int tiles_y = (nvalid + TH - 1) / TH;
+  const int64_t tiles = int64_t(tiles_x) * tiles_y;
+  // Work items: enough waves to fill 256 CUs several times over, and short
+  // enough that the dispatch tail stays small.
+  int32_t chunk = ctx->chunk;
+  if (chunk <= 0) {
+    const int64_t want_items = 256 * 8 * 16;
+    int64_t n_chunks = std::max<int64_t>(1, (want_items + tiles - 1) / tiles);
+    n_chunks = std::min<int64_t>(n_chunks, spp);
+    chunk = int32_t((spp + n_chunks - 1) / n_chunks);
+    chunk = std::max(chunk, std::min<int32_t>(spp, 32));  // keep items long enough to amortise the flush
+  }
+  chunk = std::min(chunk, spp);
+  const int32_t n_chunks = (spp + chunk - 1) / chunk;
+  const int64_t items = tiles * n_chunks;
+  if (items > int64_t(INT32_MAX) - kWavesPerBlock) return set_error(RT_EINVAL, "too many work items");
+  RenderArgs a;
+  a.cam = cam_f(cam);
+  a.n = ctx->n;
+  a.W = W; a.H = H; a.spp = spp; a.max_depth = max_depth; a.seed = seed;
+  a.row0 = row0; a.row_step = row_step; a.nrows_valid = nvalid;
+  a.tiles_x = tiles_x; a.chunk = chunk; a.n_chunks = n_chunks; a.n_items = int32_t(items);
+  const bool chunked = n_chunks > 1;
+  const size_t n_valid_out = size_t(nvalid) * W * 3;
+  if (chunked) {
+    if (ctx->accum_cap < n_valid_out) {
+      int rc = dev_alloc(&ctx->accum, n_valid_out);
+      if (rc) { ctx->accum_cap = 0; return rc; }
+      ctx->accum_cap = n_valid_out;
+    }
+    HIP_TRY(hipMemsetAsync(ctx->accum, 0, n_valid_out * sizeof(unsigned long long), st));
+  }
+  const dim3 grid(unsigned((items + kWavesPerBlock - 1) / kWavesPerBlock));
+  switch (TW) {
+    case 8: launch_tw<8>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
+    case 16: launch_tw<16>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
+    case 32: launch_tw<32>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
+    default: launch_tw<64>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
+  }
+  HIP_TRY(hipGetLastError());
+  if (chunked) {
+    hipLaunchKernelGGL(finalize_kernel, dim3(unsigned((n_valid_out + 255) / 256)), dim3(256), 0, st, ctx->accum,
+                       strip, n_valid_out);
+    HIP_TRY(hipGetLastError());
+  }
+  (void)n_out;
+  return RT_OK;
+}
+
+}  // namespace
+
+RTMI_EXPORT int rt_render_rows(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t spp,
+                               int32_t max_depth, uint64_t seed, int32_t row0, int32_t row_step, int32_t nrows,
+                               float *dev_strip, void *stream) {
+  int rc = check_render_args(ctx, cam, W, H, spp, max_depth);
+  if (rc) return rc;
+  if (row0 < 0 || row_step < 1 || nrows < 0 || (nrows > 0 && !dev_strip))
+    return set_error(RT_EINVAL, "rt_render_rows: bad row set");
+  DeviceGuard guard(ctx->device);
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  return render_rows_impl(ctx, cam, W, H, spp, max_depth, seed, row0, row_step, nrows, dev_strip, st);
+}
+
+RTMI_EXPORT int rt_ctx_synchronize(rt_ctx *ctx) {
+  if (!ctx) return set_error(RT_EINVAL, "null ctx");
+  DeviceGuard guard(ctx->device);
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_render(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t spp, int32_t max_depth,
+                          uint64_t seed, float *sum) {
+  int rc = check_render_args(ctx, cam, W, H, spp, max_depth);
+  if (rc) return rc;
+  if (!sum) return set_error(RT_EINVAL, "null output");
+  DeviceGuard guard(ctx->device);
+  const size_t n = size_t(W) * H * 3;
+  if (ctx->scratch_cap < n) {
+    if ((rc = dev_alloc(&ctx->scratch, n))) { ctx->scratch_cap = 0; return rc; }
+    ctx->scratch_cap = n;
+  }
+  if ((rc = render_rows_impl(ctx, cam, W, H, spp, max_depth, seed, 0, 1, H, ctx->scratch, ctx->stream))) return rc;
+  HIP_TRY(hipMemcpyAsync(sum, ctx->scratch, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_replay_worker(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t spp,
+                                 int32_t max_depth, int32_t n_jobs, const int32_t *job_ranges, const int32_t *streams,
+                                 const int64_t *stream_offsets, double *host_sums, int64_t *draws_used) {
+  int rc = check_render_args(ctx, cam, W, H, spp, max_depth);
+  if (rc) return rc;
+  if (max_depth > kMaxReplayDepth) return set_error(RT_EINVAL, "replay max_depth must be <= %d", kMaxReplayDepth);
+  if (n_jobs <= 0 || !job_ranges || !stream_offsets || !host_sums || !draws_used)
+    return set_error(RT_EINVAL, "rt_replay_worker: bad argument");
+  std::vector<int64_t> out_offs(n_jobs + 1, 0);
+  for (int k = 0; k < n_jobs; k++) {
+    const int s = job_ranges[2 * k], e = job_ranges[2 * k + 1];
+    if (s < 0 || e < s || int64_t(e) > int64_t(W) * H) return set_error(RT_EINVAL, "job %d: bad range", k);
+    if (stream_offsets[k + 1] < stream_offsets[k]) return set_error(RT_EINVAL, "job %d: bad stream offsets", k);
+    out_offs[k + 1] = out_offs[k] + 3 * int64_t(e - s);
+  }
+  const int64_t n_stream = stream_offsets[n_jobs];
+  DeviceGuard guard(ctx->device);
+  int32_t *d_ranges = nullptr, *d_streams = nullptr;
+  int64_t *d_offs = nullptr, *d_oo = nullptr, *d_used = nullptr;
+  double *d_out = nullptr;
+  auto cleanup = [&]() {
+    for (void *p : {(void *)d_ranges, (void *)d_streams, (void *)d_offs, (void *)d_oo, (void *)d_used, (void *)d_out})
+      if (p) (void)hipFree(p);
+  };
+  if ((rc = dev_alloc(&d_ranges, 2 * size_t(n_jobs))) || (rc = dev_alloc(&d_streams, size_t(n_stream))) ||
+      (rc = dev_alloc(&d_offs, size_t(n_jobs) + 1)) || (rc = dev_alloc(&d_oo, size_t(n_jobs) + 1)) ||
+      (rc = dev_alloc(&d_used, size_t(n_jobs))) || (rc = dev_alloc(&d_out, size_t(out_offs[n_jobs])))) {
+    cleanup();
+    return rc;
+  }
+  hipError_t e = hipSuccess;
+  auto chk = [&](hipError_t x) { if (e == hipSuccess) e = x; };
+  chk(hipMemcpy(d_ranges, job_ranges, 2 * size_t(n_jobs) * sizeof(int32_t), hipMemcpyHostToDevice));
+  if (n_stream > 0 && streams) chk(hipMemcpy(d_streams, streams, size_t(n_stream) * sizeof(int32_t), hipMemcpyHostToDevice));
+  chk(hipMemcpy(d_offs, stream_offsets, (size_t(n_jobs) + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  chk(hipMemcpy(d_oo, out_offs.data(), (size_t(n_jobs) + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  ReplayArgs a;
+  a.cam = cam_d(cam);
+  a.n = ctx->n; a.W = W; a.H = H; a.spp = spp; a.max_depth = max_depth; a.n_jobs = n_jobs;
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(replay_kernel, dim3((n_jobs + 63) / 64), dim3(64), 0, ctx->stream, ctx->geom64, ctx->sh064,
+                       ctx->sh164, a, d_ranges, d_streams, d_offs, d_oo, d_out, d_used);
+    chk(hipGetLastError());
+    chk(hipStreamSynchronize(ctx->stream));
+    chk(hipMemcpy(host_sums, d_out, size_t(out_offs[n_jobs]) * sizeof(double), hipMemcpyDeviceToHost));
+    chk(hipMemcpy(draws_used, d_used, size_t(n_jobs) * sizeof(int64_t), hipMemcpyDeviceToHost));
+  }
+  cleanup();
+  if (e != hipSuccess) return set_error(RT_EHIP, "rt_replay_worker: %s", hipGetErrorString(e));
+  for (int k = 0; k < n_jobs; k++)
+    if (draws_used[k] < 0) return set_error(RT_ESTREAM, "job %d ran out of stream values", k);
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_ctx_last_segments(rt_ctx *ctx, uint64_t *segments) {
+  if (!ctx || !segments) return set_error(RT_EINVAL, "null argument");
+  DeviceGuard guard(ctx->device);
+  hipStream_t st = ctx->last_stream ? ctx->last_stream : ctx->stream;
+  unsigned long long v = 0;
+  HIP_TRY(hipMemcpyAsync(&v, ctx->segments, sizeof v, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  *segments = v;
+  return RT_OK;
+}

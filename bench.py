@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""bench.py — Msamples/s on the RTIOW final scene (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+One step = one full render of the config-2 workload: the final random-spheres
+scene (487 spheres, glibc seed 1 as the reference), 1200x800, 500 spp, depth
+50.  At N > 1 the image is split over ranks by interleaved rows (row j -> rank
+j % N), each rank renders its strip on its own GPU, and the strips are
+gathered to rank 0 with ONE RCCL gather (torch.distributed "nccl" = RCCL)
+inside the timed region.  Total work is fixed as N grows: scaling "strong".
+value = W*H*spp*K / max-over-ranks(wall time of K steps) / 1e6.
+
+roofline: FP32 VALU bound.  achieved = segments * 18 * 487 FLOP per launch
+(18 flops per ray-sphere test, brute force over 487 spheres;
+segments = world.hit calls, counted exactly on the GPU) / mean launch time
+from HIP events on the launch stream; peak = 157.3 TFLOP/s FP32 vector.
+cpu_baseline: the reference itself (oracle/_ref/ref_harness: worker() at -O2,
+16 std::threads as the reference's concurrency) on a bounded sample, rank 0,
+N = 1 only.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+W, H, SPP, DEPTH, SEED = 1200, 800, 500, 50, 1984
+FLOP_PER_SPHERE_TEST = 18
+PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector (MI355X_MICROARCH.md)
+PUBLISHED_CPU_MSPS = 0.1189  # README.md:16-19: rt_in_one_weekend, 1200x800x500, 16 threads, 4036.1 s
+METRIC = "Msamples/sec (pixels x spp) on RTIOW final scene"
+
+
+def cpu_baseline(threads=16):
+    """The reference's own worker() (oracle/_ref/ref_harness bench) on a
+    bounded sample: full 1200x800 image at 4 spp (~3.8 M samples)."""
+    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    spp = 4
+    if os.path.exists(harness):
+        try:
+            out = subprocess.run([harness, "bench", str(threads), str(W), str(H), str(spp), str(DEPTH)],
+                                 capture_output=True, text=True, timeout=300, check=True).stdout
+            r = json.loads(out.strip().splitlines()[-1])
+            return {"value": round(r["msamples_per_s"], 5), "unit": "Msamples/s", "cores": threads, "kind": "reference",
+                    "sample": f"reference worker() g++ -O2, {threads} std::threads, final scene {W}x{H}x{spp}spp depth {DEPTH} "
+                              f"({r['seconds']:.1f} s wall)"}
+        except Exception as e:  # fall through to the port
+            print(f"bench: reference harness failed: {e}", file=sys.stderr)
+    try:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_py as O
+        import ctypes
+
+        sc, _ = O.final_scene()
+        cam = O.final_camera(1.5)
+        rows = 40
+        os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+        t0 = time.perf_counter()
+        O.fast_render(sc, cam, W, H, spp, DEPTH, SEED, row0=0, row_step=H // rows, nrows=rows)
+        dt = time.perf_counter() - t0
+        return {"value": round(rows * W * spp / dt / 1e6, 5), "unit": "Msamples/s", "cores": int(os.environ["OMP_NUM_THREADS"]),
+                "kind": "port", "sample": f"oracle fast-mode C restatement, {rows} rows x {W} x {spp} spp"}
+    except Exception as e:
+        print(f"bench: cpu baseline unavailable: {e}", file=sys.stderr)
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--tile-w", type=int, default=8)
+    ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import a_dive_into_ray_tracing_amd as rt
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE {world_size}", file=sys.stderr)
+    N = world_size
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if N > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    world = rt.random_scene()
+    cam = rt.final_camera(W / H)
+    r = rt.Renderer(world, local_rank, tile_w=args.tile_w, chunk=args.chunk)
+    nrows = (H + N - 1) // N
+    strip = torch.empty((nrows, W, 3), dtype=torch.float32, device=dev)
+    gather = [torch.empty_like(strip) for _ in range(N)] if (N > 1 and rank == 0) else None
+    stream = torch.cuda.current_stream(dev)
+
+    ev = []
+
+    def step(record):
+        if record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        r.render_rows(cam, W, H, SPP, DEPTH, SEED, rank, N, nrows, strip.data_ptr(), stream.cuda_stream)
+        if record:
+            e1.record(stream)
+            ev.append((e0, e1))
+        if N > 1:  # the single exchange step: strips -> rank 0 over RCCL/xGMI
+            dist.gather(strip, gather_list=gather, dst=0)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    if N > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    if N > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if N > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    segs = r.last_segments()  # this rank's strip, last render
+    if N > 1:
+        t = torch.tensor([segs], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        total_segs = float(t.item())
+        km = torch.tensor([kernel_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        kernel_ms_max = float(km.item())
+    else:
+        total_segs, kernel_ms_max = float(segs), kernel_ms
+
+    if rank == 0:
+        samples = W * H * SPP
+        value = samples * args.steps / elapsed / 1e6
+        flop_rank = segs * FLOP_PER_SPHERE_TEST * len(world)  # this rank's launch
+        achieved = flop_rank / (kernel_ms * 1e-3) / 1e12
+        traffic = None
+        pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": N,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(value / PUBLISHED_CPU_MSPS, 1),
+            "dtype": "f32",
+            "data": "synthetic: RTIOW final scene regenerated from glibc rand() seed 1 (487 spheres, = reference)",
+            "config": {
+                "workload": "rtiow_final_1200x800_500spp_depth50",
+                "width": W, "height": H, "spp": SPP, "max_depth": DEPTH, "seed": SEED, "spheres": len(world),
+                "partition": "interleaved rows, one RCCL gather" if N > 1 else "single GPU",
+                "tile": f"{args.tile_w}x{64 // args.tile_w}",
+            },
+            "roofline": {
+                "bound": "valu",
+                "achieved": round(achieved, 3),
+                "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                "traffic": traffic,
+                "flop_per_launch": flop_rank,
+                "segments_per_launch": segs,
+                "segments_per_sample": round(total_segs / samples, 4),
+                "kernel_ms": round(kernel_ms, 3),
+                "kernel_ms_max_rank": round(kernel_ms_max, 3),
+            },
+            "vs_baseline_ref": "published CPU rt_in_one_weekend 0.1189 Msamples/s (README.md:16-19)",
+        }
+        if N == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(line), flush=True)
+    r.close()
+    if N > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

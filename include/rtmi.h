@@ -1,0 +1,160 @@
+/* include/rtmi.h — C ABI of librtmi.so, the MI355X-native path tracer.
+ *
+ * Drop-in boundary for the reference's per-pixel sample loop
+ * (xyloid/a_dive_into_ray_tracing, rt_in_one_weekend/).  The reference has no
+ * FFI; its de-facto interface is the C++ call
+ *     worker(start, end, std::ref(img), W, H, world, cam, spp, max_depth)
+ *                                               rt_in_one_weekend/main.cpp:267-290
+ * fed by hittable_list::objects (hittable_list.h:16-17) and the public camera
+ * fields (camera.h:64-70), and followed by the P3 writer (color.h:14-28 via
+ * main.cpp:344-355).  Every entry point below names the reference code it
+ * replaces.  Plain pointers and sizes only; no C++ or torch types.
+ *
+ * Conventions
+ *  - Every int-returning call returns RT_OK (0) or a negative RT_E* code and
+ *    never exits the process (the CUDA reference exit(99)s: final.cu:13-24).
+ *    rt_last_error() describes the last failure of the calling thread.
+ *  - Inputs are copied; the caller keeps ownership.  Host outputs are caller
+ *    allocated.  Image buffers are W*H*3 floats, index (j*W + i)*3 + c, row
+ *    j = 0 at the BOTTOM (main.cpp:274-275), holding per-pixel SUMS over the
+ *    samples (main.cpp:276-285) — not means.
+ *  - Scene and camera are given in double (the reference's type) and rounded
+ *    to float on entry; the render computes in float.
+ *  - The image is a pure function of (scene, camera, W, H, spp, max_depth,
+ *    seed): independent of tiling, scheduling, row partition and GPU count.
+ *  - There is no CPU fallback: without a usable gfx950 device every render
+ *    call fails with RT_ENODEVICE.
+ */
+#ifndef RTMI_H
+#define RTMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTMI_VERSION_MAJOR 0
+#define RTMI_VERSION_MINOR 1
+
+enum {
+  RT_OK = 0,
+  RT_EINVAL = -1,       /* bad argument                                   */
+  RT_EHIP = -2,         /* HIP runtime failure                            */
+  RT_ENODEVICE = -3,    /* no HIP device / device index out of range      */
+  RT_EUNSUPPORTED = -4, /* object/material type the path cannot render    */
+  RT_ENOMEM = -5,       /* host or device allocation failed               */
+  RT_ERCCL = -6,        /* RCCL failure (multi-GPU render)                */
+  RT_EIO = -7,          /* file output failed                             */
+  RT_ESTREAM = -8       /* replay stream exhausted                        */
+};
+
+/* material kinds, material.h:15-97 */
+enum { RT_MAT_LAMBERTIAN = 0, RT_MAT_METAL = 1, RT_MAT_DIELECTRIC = 2 };
+
+/* hittable_list of spheres (hittable_list.h:16-17, sphere.h:15-19). */
+typedef struct rt_scene {
+  int32_t n;                   /* number of spheres                               */
+  const double *center_radius; /* 4n: cx cy cz radius (negative radius allowed)   */
+  const int32_t *mat_kind;     /* n: RT_MAT_*                                     */
+  const double *mat_params;    /* 4n: albedo r g b, then fuzz (metal) | ir (diel.) */
+} rt_scene;
+
+/* camera public fields, camera.h:64-70 */
+typedef struct rt_camera {
+  double origin[3];
+  double lower_left_corner[3];
+  double horizontal[3];
+  double vertical[3];
+  double u[3], v[3], w[3];
+  double lens_radius;
+} rt_camera;
+
+typedef struct rt_ctx rt_ctx; /* one device, its stream, the resident scene */
+
+/* ---------------- host helpers (no GPU needed) ------------------------- */
+const char *rt_last_error(void);
+int rt_version(void); /* (major << 16) | minor */
+
+/* camera::camera(lookfrom, lookat, vup, vfov, aspect, aperture, focus_dist)
+ * camera.h:8-45, evaluated in double exactly as the reference does. */
+int rt_camera_init(rt_camera *cam, const double lookfrom[3], const double lookat[3],
+                   const double vup[3], double vfov_deg, double aspect_ratio,
+                   double aperture, double focus_dist);
+
+/* random_scene() main.cpp:86-131 (final random-spheres scene), generated from
+ * glibc's rand() stream seeded with `glibc_seed` (the reference never seeds:
+ * 1) with GCC's draw order, so it equals the reference's 487 objects.
+ * Writes up to `cap` spheres; *n_out = count.  RT_EINVAL if cap too small. */
+int rt_scene_random(uint32_t glibc_seed, double *center_radius, int32_t *mat_kind,
+                    double *mat_params, int32_t cap, int32_t *n_out);
+/* learn() scene main.cpp:198-210 (config 1, five spheres incl. radius -0.4). */
+int rt_scene_learn(double *center_radius, int32_t *mat_kind, double *mat_params, int32_t cap,
+                   int32_t *n_out);
+
+/* write_color(out, sum, spp) color.h:14-28 over the image, top row first
+ * (main.cpp:344-355).  path "-" = stdout.  binary != 0 writes P6 instead of P3
+ * with the same 8-bit values. */
+int rt_write_ppm(const char *path, const float *sum, int32_t W, int32_t H, int32_t spp,
+                 int32_t binary);
+/* Same quantisation into rgb[W*H*3] bytes, top row first. */
+int rt_quantize(const float *sum, int32_t W, int32_t H, int32_t spp, uint8_t *rgb);
+
+/* ---------------- device ----------------------------------------------- */
+int rt_device_count(int32_t *n);
+/* Create a context on HIP device `device` (its own non-blocking stream). */
+int rt_ctx_create(int32_t device, rt_ctx **out);
+int rt_ctx_destroy(rt_ctx *ctx);
+/* Upload the scene (replaces the per-thread copies of `world`,
+ * main.cpp:331-333).  Synchronous; O(n). */
+int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene);
+/* Tuning: tile_w in {8, 16, 32, 64} (tile = tile_w x 64/tile_w pixels per
+ * wavefront); chunk = samples per work item (0 = automatic).  Neither
+ * changes the image. */
+int rt_ctx_set_tuning(rt_ctx *ctx, int32_t tile_w, int32_t chunk);
+
+/* The whole image: replaces the 16-thread worker() block main.cpp:313-338.
+ * Synchronous; `sum` is a HOST buffer of W*H*3 floats. */
+int rt_render(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t spp,
+              int32_t max_depth, uint64_t seed, float *sum);
+
+/* Rows row0, row0+row_step, ..., (nrows of them) into a DEVICE strip buffer
+ * dev_strip[nrows*W*3] (strip row r = image row row0 + r*row_step; rows past
+ * H are zero-filled).  Asynchronous on `stream` (hipStream_t; NULL = the
+ * context's stream).  This is the per-GPU unit of the multi-GPU row
+ * partition.  dev_strip must stay valid until the stream
+ * reaches the end of this call's work. */
+int rt_render_rows(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t spp,
+                   int32_t max_depth, uint64_t seed, int32_t row0, int32_t row_step,
+                   int32_t nrows, float *dev_strip, void *stream);
+/* Number of world.hit calls (path segments) of the context's
+ * last render, counted on the GPU; waits for that render to finish.  The
+ * algorithmic work of a render is segments * 18 * n_spheres FLOP. */
+int rt_ctx_last_segments(rt_ctx *ctx, uint64_t *segments);
+/* Block until the context's stream is idle. */
+int rt_ctx_synchronize(rt_ctx *ctx);
+
+/* Exact replay (validation): runs n_jobs reference worker(start, end, ...)
+ * calls (main.cpp:267-290) on the GPU in DOUBLE with the reference's op
+ * order, consuming for job k the supplied glibc rand() values
+ * streams[stream_offsets[k] .. stream_offsets[k+1]) in place of rand().
+ * job_ranges = {start0, end0, start1, end1, ...}; host_sums receives
+ * Σ(end-start)*3 doubles in job order; draws_used[k] = values consumed.
+ * max_depth <= 64.  RT_ESTREAM if a job runs out of stream values. */
+int rt_replay_worker(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t spp,
+                     int32_t max_depth, int32_t n_jobs, const int32_t *job_ranges,
+                     const int32_t *streams, const int64_t *stream_offsets, double *host_sums,
+                     int64_t *draws_used);
+
+/* Multi-GPU render in one process (the C++ drop-in path): rows interleaved
+ * over n_gpus devices (row j -> device j % n_gpus), one RCCL gather of the
+ * per-device strips to device 0 over xGMI, un-permuted into `sum` (HOST,
+ * W*H*3).  n_gpus = 0 means all visible devices.  Same image as rt_render. */
+int rt_render_multi(const rt_scene *scene, const rt_camera *cam, int32_t W, int32_t H,
+                    int32_t spp, int32_t max_depth, uint64_t seed, int32_t n_gpus, float *sum);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTMI_H */

@@ -1,0 +1,234 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle.
+
+Three tiers:
+  1. exact replay: the double-precision kernel instantiation, fed the
+     reference's own rand() stream, reproduces the reference's KATs and
+     single-threaded images BIT-EXACTLY;
+  2. fast path: the production float kernel equals the oracle's fast-mode
+     restatement BIT-EXACTLY (stricter than the 1e-4 per-channel tolerance
+     north_star states) at sizes the oracle finishes in seconds, over every
+     tile shape, chunking, edge tiles and depth edge cases;
+  3. statistics: at config 2 (1200x800x500) the image sits at the reference's
+     own Monte-Carlo noise floor against gallery/final.png, the reference's
+     output (BASELINE.md §5 thresholds).
+Plus size-independent properties at full size: determinism and partition /
+tiling invariance.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import a_dive_into_ray_tracing_amd as rt
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+GOLD = O.GOLDEN
+SEED = 1984
+
+
+@pytest.fixture(scope="module")
+def final_world():
+    return rt.random_scene()
+
+
+@pytest.fixture(scope="module")
+def final_renderer(final_world):
+    r = rt.Renderer(final_world, 0)
+    yield r
+    r.close()
+
+
+@pytest.fixture(scope="module")
+def learn_renderer():
+    r = rt.Renderer(rt.learn_scene(), 0)
+    yield r
+    r.close()
+
+
+def o_cam(cam):
+    c = O.OrCamera()
+    C.memmove(C.byref(c), C.byref(cam), C.sizeof(c))
+    return c
+
+
+def o_scene(world):
+    return O.Scene(world.center_radius, world.mat_kind, world.mat_params)
+
+
+# ------------------------------------------------------------ tier 1 -------
+def glibc_stream(seed, n, skip_scene=False):
+    g = O.OrGlibc()
+    O.lib().or_glibc_seed(C.byref(g), seed)
+    if skip_scene:  # the final scene's draws come first in a fresh process
+        geom, kind, mat = np.zeros(4 * 600), np.zeros(600, np.int32), np.zeros(4 * 600)
+        O.lib().or_final_scene(C.byref(g), O.dptr(geom), kind.ctypes.data_as(O._ip), O.dptr(mat), 600)
+    return np.array([O.lib().or_glibc_rand(C.byref(g)) for _ in range(n)], np.int32)
+
+
+@pytest.mark.parametrize("name", ["final", "learn"])
+def test_exact_replay_reproduces_reference_kats(name, final_renderer, learn_renderer):
+    r = final_renderer if name == "final" else learn_renderer
+    cam = rt.final_camera() if name == "final" else rt.learn_camera()
+    lines = open(os.path.join(GOLD, f"kats_{name}.txt")).read().split("\n")
+    n, W, H = map(int, lines[0].split())
+    kats = [ln.split() for ln in lines[1 : 1 + n]]
+    jobs, streams = [], []
+    for t in kats:
+        k, i, j = int(t[0]), int(t[1]), int(t[2])
+        jobs.append((j * W + i, j * W + i + 1))
+        streams.append(glibc_stream(k, 2048))
+    out, used = r.replay_worker(cam, W, H, 1, 50, jobs, streams)
+    out = out.reshape(n, 3)
+    for q, t in enumerate(kats):
+        assert out[q].tolist() == [float(x) for x in t[3:6]], t[0]
+        assert streams[q][used[q]] == int(t[6]), t[0]  # the next rand() the reference drew
+
+
+@pytest.mark.parametrize("name,W,H,S", [("final", 24, 16, 8), ("learn", 32, 18, 16)])
+def test_exact_replay_reproduces_reference_image(name, W, H, S, final_renderer, learn_renderer):
+    r = final_renderer if name == "final" else learn_renderer
+    cam = rt.final_camera(W / H) if name == "final" else rt.learn_camera(W / H)
+    stream = glibc_stream(1, 200_000, skip_scene=(name == "final"))
+    out, used = r.replay_worker(cam, W, H, S, 50, [(0, W * H)], [stream])
+    gold = np.fromfile(os.path.join(GOLD, f"image_{name}_{W}x{H}x{S}.f64"), dtype="<f8")
+    assert np.array_equal(out, gold)
+
+
+# ------------------------------------------------------------ tier 2 -------
+@pytest.mark.parametrize("tile_w", [8, 16, 32, 64])
+@pytest.mark.parametrize("chunk", [0, 3, 1000])
+def test_fast_kernel_bit_exact_vs_oracle_final(tile_w, chunk, final_world, final_renderer):
+    W, H, S = 48, 32, 8
+    cam = rt.final_camera(W / H)
+    final_renderer.set_tuning(tile_w, chunk)
+    got = final_renderer.render(cam, W, H, S, 50, SEED)
+    final_renderer.set_tuning(8, 0)
+    want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
+    assert np.array_equal(got, want), np.abs(got - want).max()
+
+
+@pytest.mark.parametrize("W,H,S,depth", [(37, 23, 5, 50), (64, 36, 16, 50), (20, 11, 3, 1), (16, 16, 4, 2), (9, 7, 1, 50)])
+def test_fast_kernel_bit_exact_vs_oracle_learn(W, H, S, depth, learn_renderer):
+    """Edge tiles (W, H not multiples of the tile), spp=1, max_depth 1 and 2,
+    the hollow negative-radius sphere."""
+    world = rt.learn_scene()
+    cam = rt.learn_camera(W / H)
+    got = learn_renderer.render(cam, W, H, S, depth, SEED)
+    want = O.fast_render(o_scene(world), o_cam(cam), W, H, S, depth, SEED)
+    assert np.array_equal(got, want), np.abs(got - want).max()
+
+
+def test_max_depth_zero_is_black(learn_renderer):
+    got = learn_renderer.render(rt.learn_camera(), 16, 9, 4, 0, SEED)
+    assert not got.any()
+
+
+def test_seed_changes_image(learn_renderer):
+    cam = rt.learn_camera(2.0)
+    a = learn_renderer.render(cam, 32, 16, 4, 50, 1)
+    b = learn_renderer.render(cam, 32, 16, 4, 50, 2)
+    assert not np.array_equal(a, b)
+
+
+def test_config1_fast_vs_oracle_bit_exact(learn_renderer):
+    """Config 1 (400x225x100, learn) whole image vs the fast-mode oracle."""
+    world = rt.learn_scene()
+    cam = rt.learn_camera(400 / 225)
+    got = learn_renderer.render(cam, 400, 225, 100, 50, SEED)
+    want = O.fast_render(o_scene(world), o_cam(cam), 400, 225, 100, 50, SEED)
+    assert np.array_equal(got, want)
+    # tolerance stated by north_star, for the record: <= 1e-4 per channel on sum/spp
+    assert np.abs(got / 100 - want / 100).max() <= 1e-4
+
+
+def test_rows_strips_equal_full_image(final_renderer):
+    torch = pytest.importorskip("torch")
+    W, H, S, G = 40, 30, 4, 4
+    cam = rt.final_camera(W / H)
+    full = final_renderer.render(cam, W, H, S, 50, SEED)
+    nrows = (H + G - 1) // G
+    dev = torch.device("cuda", 0)
+    for g in range(G):
+        strip = torch.full((nrows, W, 3), -1.0, dtype=torch.float32, device=dev)
+        final_renderer.render_rows(cam, W, H, S, 50, SEED, g, G, nrows, strip.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        s = strip.cpu().numpy()
+        for k in range(nrows):
+            j = g + k * G
+            if j < H:
+                assert np.array_equal(s[k], full[j]), (g, k)
+            else:
+                assert not s[k].any()
+
+
+def test_render_multi_one_gpu_equals_render(final_world, final_renderer):
+    W, H, S = 40, 30, 4
+    cam = rt.final_camera(W / H)
+    a = final_renderer.render(cam, W, H, S, 50, SEED)
+    b = rt.render_multi(W, H, S, 50, final_world, cam, SEED, n_gpus=1)
+    assert np.array_equal(a, b)
+
+
+# ---------------------------------------------------- full-size properties -
+@pytest.fixture(scope="module")
+def config2(final_renderer):
+    cam = rt.final_camera(1.5)
+    final_renderer.set_tuning(8, 0)
+    img = final_renderer.render(cam, 1200, 800, 500, 50, SEED)
+    return cam, img
+
+
+def test_config2_deterministic_and_tiling_invariant(config2, final_renderer):
+    cam, img = config2
+    final_renderer.set_tuning(64, 100)
+    again = final_renderer.render(cam, 1200, 800, 500, 50, SEED)
+    final_renderer.set_tuning(8, 0)
+    assert np.array_equal(img, again)
+
+
+def test_config2_sampled_pixels_bit_exact_vs_oracle(config2, final_world):
+    """A strip of config 2 (rows 0, 97, 194, ...: every 97th row, 9 rows)
+    against the oracle at full width and spp."""
+    cam, img = config2
+    want = O.fast_render(o_scene(final_world), o_cam(cam), 1200, 800, 500, 50, SEED, row0=0, row_step=97, nrows=9)
+    assert np.array_equal(img[0::97][:9], want)
+
+
+def _png_rgb(path):
+    from PIL import Image
+
+    return np.asarray(Image.open(path).convert("RGB"), dtype=np.float64)
+
+
+def test_config2_statistics_vs_reference_gallery(config2):
+    """reference-vs-reference noise at config 2 is bias 0.0014,
+    MAE 1.064, RMSE 1.795, 40x40-tile max |d| 0.254 levels.  Thresholds from
+    SURVEY §8(c): |bias| < 0.05, MAE <= 1.2, RMSE <= 2.0, tile max <= 0.4."""
+    _, img = config2
+    ours = rt.quantize(img, 500).astype(np.float64)
+    ref = _png_rgb(os.path.join(GOLD, "gallery_final.png"))
+    d = ours - ref
+    bias, mae, rmse = d.mean(), np.abs(d).mean(), np.sqrt((d * d).mean())
+    tiles = ours.reshape(20, 40, 30, 40, 3).mean(axis=(1, 3))
+    tile_max = np.abs(tiles - np.load(os.path.join(GOLD, "gallery_final_tiles40.npy"))).max()
+    print(f"config2 vs gallery: bias {bias:.4f} MAE {mae:.3f} RMSE {rmse:.3f} tile max {tile_max:.3f}")
+    assert abs(bias) < 0.05 and mae <= 1.2 and rmse <= 2.0 and tile_max <= 0.4
+
+
+def test_config1_statistics_vs_reference_image(learn_renderer):
+    """Config 1 GPU image vs the reference's config-1 image, against the
+    reference's own noise (ref mode, a different rand() seed)."""
+    cam = rt.learn_camera(400 / 225)
+    ours = rt.quantize(learn_renderer.render(cam, 400, 225, 100, 50, SEED), 100).astype(np.float64)
+    raw = open(os.path.join(GOLD, "learn_400x225x100.ppm"), "rb").read()
+    gold = np.frombuffer(raw[len(b"P6\n400 225\n255\n"):], np.uint8).reshape(225, 400, 3).astype(np.float64)
+    g = O.OrGlibc()
+    O.lib().or_glibc_seed(C.byref(g), 7)
+    other, _ = O.ref_worker(O.learn_scene(), O.learn_camera(400 / 225), 400, 225, 100, 50, 0, 400 * 225, g)
+    noise = rt.quantize(other.reshape(225, 400, 3).astype(np.float32), 100).astype(np.float64)
+    floor = np.sqrt(((noise - gold) ** 2).mean())
+    rmse = np.sqrt(((ours - gold) ** 2).mean())
+    print(f"config1 RMSE ours {rmse:.3f} vs reference-vs-reference {floor:.3f}")
+    assert rmse <= 1.15 * floor and abs((ours - gold).mean()) < 0.1

@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "librtmi.so")
+LIB_PATH = os.environ.get("RTMI_LIBRARY") or os.path.join(PKG_DIR, "lib", "librtmi.so")
 
 RT_OK = 0
 ERRORS = {
@@ -77,6 +77,15 @@ def load():
     """Load librtmi.so once; raises if it has not been built."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch's wheel bundles libamdhip64 /
+        # libhsa-runtime64 / librccl under the same SONAMEs as /opt/rocm.  If
+        # torch is importable, load it first so librtmi.so binds to the copy
+        # already in the process (device pointers and streams are then shared
+        # with torch); loading ours first would leave torch a second runtime.
+        try:
+            import torch  # noqa: F401
+        except Exception:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"librtmi.so not built at {LIB_PATH}: run `make -C a_dive_into_ray_tracing_amd/csrc`")
         L = C.CDLL(LIB_PATH)

@@ -233,6 +233,71 @@ __device__ __forceinline__ int32_t hit_world(const SceneView<R> &sc, V3<R> o, V3
   return best;
 }
 
+// The fast path's form of hit_world: spheres in groups of G.  The group's
+// {centre, r^2} are wave-uniform scalar loads (s_load_dwordx16 for G = 4),
+// the G discriminants are computed branch-free (independent chains), and the
+// wave takes ONE branch per group when no lane has a candidate — the common
+// case.  The candidate test is the sign-bit form of
+//     !(disc < 0) && !(hb >= 0 && cc >= 0)
+// (skips a subset of what that skips, so every skip stays result-preserving,
+// DESIGN.md §3.2).  Candidates are resolved in sphere order, so ties and the
+// shrinking t_max behave exactly as the sequential loop of hit_world above.
+template <int G>
+__device__ __forceinline__ int32_t hit_world_grouped(const float4 *__restrict__ geom, int32_t n, V3<float> o,
+                                                     V3<float> d, float &t_hit) {
+  const float a = dot<true>(d, d);
+  const float na = -a;  // na*cc == -(a*cc) exactly: saves the negation per sphere
+  const float inv_a = 1.0f / a;
+  const float t_min = 0.001f;
+  float t_max = INFINITY;
+  int32_t best = -1;
+  auto resolve = [&](int32_t idx, float hb, float disc) {
+    const float sq = dsqrt(disc);
+    float root = (-hb - sq) * inv_a;
+    bool ok = !(root < t_min || t_max < root);
+    if (!ok) {
+      root = (-hb + sq) * inv_a;
+      ok = !(root < t_min || t_max < root);
+    }
+    if (ok) {
+      t_max = root;
+      best = idx;
+    }
+  };
+  auto test = [&](const float4 s, float &hb, float &disc) -> int {
+    const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;
+    hb = __builtin_fmaf(ocz, d.z, __builtin_fmaf(ocy, d.y, ocx * d.x));
+    const float cc = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - s.w;
+    disc = __builtin_fmaf(hb, hb, na * cc);
+    return (__float_as_int(hb) | __float_as_int(cc)) & ~__float_as_int(disc);  // < 0: candidate
+  };
+  int32_t k = 0;
+  for (; k + G <= n; k += G) {
+    float4 s[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) s[g] = geom[k + g];
+    float hb[G], disc[G];
+    int ci[G];
+    int any = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      ci[g] = test(s[g], hb[g], disc[g]);
+      any |= ci[g];
+    }
+    if (any < 0) {
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (ci[g] < 0) resolve(k + g, hb[g], disc[g]);
+    }
+  }
+  for (; k < n; ++k) {
+    float hb, disc;
+    if (test(geom[k], hb, disc) < 0) resolve(k, hb, disc);
+  }
+  t_hit = t_max;
+  return best;
+}
+
 // material::scatter material.h:15-97.  Returns true if the ray scattered.
 template <bool F, class R, class G>
 __device__ __forceinline__ bool scatter(const SceneView<R> &sc, int32_t k, V3<R> din, V3<R> normal,
@@ -302,6 +367,10 @@ struct RenderArgs {
 };
 
 constexpr int kWavesPerBlock = 4;
+#ifndef RTMI_SPHERE_GROUP
+#define RTMI_SPHERE_GROUP 4
+#endif
+constexpr int kSphereGroup = RTMI_SPHERE_GROUP;
 
 __device__ __forceinline__ int64_t to_fixed(float c) { return int64_t(c * 4294967296.0f); }
 __device__ __forceinline__ float from_fixed(int64_t v) { return float(v) * 0x1p-32f; }
@@ -370,7 +439,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void render_kernel(
     if (active) {
       float t;
       ++nseg;
-      const int k = hit_world<true, float>(sc, o, d, t);
+      const int k = hit_world_grouped<kSphereGroup>(geom, a.n, o, d, t);
       if (k < 0) {
         const V3<float> sk = sky<true, float>(d);
         col = mk(T.x * sk.x, T.y * sk.y, T.z * sk.z);
@@ -383,7 +452,16 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void render_kernel(
           done = true;  // absorbed (metal below the surface): black, main.cpp:78
         } else {
           T = mk(T.x * at.x, T.y * at.y, T.z * at.z);
-          o = p;
+          // float robustness: start the next segment
+          // 2^-14 * (1 + |p|_inf) off the surface, on the side the scattered
+          // ray leaves on, so float hit-point error (~1e-6) cannot re-hit the
+          // surface just left or trap the path inside an opaque sphere.
+          float m = __builtin_fabsf(p.x);
+          if (__builtin_fabsf(p.y) > m) m = __builtin_fabsf(p.y);
+          if (__builtin_fabsf(p.z) > m) m = __builtin_fabsf(p.z);
+          float delta = 0x1p-14f * (1.0f + m);
+          if (dot<true>(nd, nrm) < 0.f) delta = -delta;
+          o = mk(__builtin_fmaf(delta, nrm.x, p.x), __builtin_fmaf(delta, nrm.y, p.y), __builtin_fmaf(delta, nrm.z, p.z));
           d = nd;
           if (++depth >= a.max_depth) done = true;  // depth exhausted: black, main.cpp:58-60
         }

@@ -105,7 +105,10 @@ def main():
     nrows = (H + N - 1) // N
     strip = torch.empty((nrows, W, 3), dtype=torch.float32, device=dev)
     gather = [torch.empty_like(strip) for _ in range(N)] if (N > 1 and rank == 0) else None
-    stream = torch.cuda.current_stream(dev)
+    # a non-default stream: the kernel, its HIP events and the RCCL gather
+    # are all ordered on it (the null stream would bypass the events)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
 
     ev = []
 

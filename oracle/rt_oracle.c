@@ -93,6 +93,7 @@ void or_fast_rng(uint64_t seed, uint64_t pixel, uint32_t sample, int32_t n, uint
 /* ---------------------------------------------------------------------- */
 /* ref instantiation: double, no FMA, glibc stream, recursion order.        */
 /* ---------------------------------------------------------------------- */
+#define RAY_OFFSET 0
 #define PFX(x) ref_##x
 #define R double
 #define MADD(a, b, c) ((a) * (b) + (c))
@@ -116,6 +117,7 @@ void or_fast_rng(uint64_t seed, uint64_t pixel, uint32_t sample, int32_t n, uint
 #undef UNI
 #undef ROOT
 #undef T_STACK
+#undef RAY_OFFSET
 
 /* ---------------------------------------------------------------------- */
 /* fast instantiation: float, fmaf policy, xoroshiro, forward product.      */
@@ -125,6 +127,7 @@ static inline float pow5f(float x) {
   float x4 = x2 * x2;
   return x4 * x;
 }
+#define RAY_OFFSET 1
 #define PFX(x) fast_##x
 #define R float
 #define MADD(a, b, c) fmaf((a), (b), (c))
@@ -231,6 +234,9 @@ void or_camera_make(or_camera *c, const double lf[3], const double la[3], const 
 /* ---------------------------------------------------------------------- */
 /* ref-mode API                                                             */
 /* ---------------------------------------------------------------------- */
+static int64_t g_ref_last_segments = 0;
+int64_t or_ref_last_segments(void) { return g_ref_last_segments; }
+
 int64_t or_ref_worker(const or_scene *s, const or_camera *c, int32_t W, int32_t H, int32_t spp,
                       int32_t max_depth, int32_t start, int32_t end, or_glibc *g, double *out) {
   ref_world w;
@@ -246,6 +252,7 @@ int64_t or_ref_worker(const or_scene *s, const or_camera *c, int32_t W, int32_t 
     o[0] = sum.x; o[1] = sum.y; o[2] = sum.z;
   }
   free(w.s);
+  g_ref_last_segments = segs;
   return g->draws - d0;
 }
 

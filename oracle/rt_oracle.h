@@ -59,6 +59,8 @@ void or_camera_make(or_camera *c, const double lookfrom[3], const double lookat[
  * out: (end-start)*3 sums.  Returns the number of rand() draws consumed. */
 int64_t or_ref_worker(const or_scene *s, const or_camera *c, int32_t W, int32_t H, int32_t spp,
                       int32_t max_depth, int32_t start, int32_t end, or_glibc *g, double *out);
+/* world.hit calls of the last or_ref_worker call (single-threaded). */
+int64_t or_ref_last_segments(void);
 /* One seeded KAT sample: srand(seed); u,v; get_ray; ray_color.  Writes the
  * colour and returns the next rand() value (main.cpp:278-281). */
 int32_t or_ref_kat(const or_scene *s, const or_camera *c, int32_t W, int32_t H, int32_t max_depth,

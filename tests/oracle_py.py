@@ -51,6 +51,7 @@ def lib():
         L.or_camera_make.argtypes = [C.POINTER(OrCamera), _dp, _dp, _dp, C.c_double, C.c_double, C.c_double, C.c_double]
         L.or_ref_worker.argtypes = [C.POINTER(OrScene), C.POINTER(OrCamera)] + [C.c_int32] * 6 + [C.POINTER(OrGlibc), _dp]
         L.or_ref_worker.restype = C.c_int64
+        L.or_ref_last_segments.restype = C.c_int64
         L.or_ref_kat.argtypes = [C.POINTER(OrScene), C.POINTER(OrCamera)] + [C.c_int32] * 5 + [C.c_uint32, _dp]
         L.or_ref_kat.restype = C.c_int32
         L.or_ref_sphere_hit.argtypes = [_dp, C.c_double, _dp, _dp, C.c_double, C.c_double, _dp, _dp, _dp, _ip]

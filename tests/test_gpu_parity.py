@@ -232,3 +232,12 @@ def test_config1_statistics_vs_reference_image(learn_renderer):
     rmse = np.sqrt(((ours - gold) ** 2).mean())
     print(f"config1 RMSE ours {rmse:.3f} vs reference-vs-reference {floor:.3f}")
     assert rmse <= 1.15 * floor and abs((ours - gold).mean()) < 0.1
+
+
+def test_segment_count_matches_oracle(final_world, final_renderer):
+    """The GPU's world.hit counter (the roofline's work unit) equals the
+    oracle's count for the same render: same paths, same lengths."""
+    W, H, S = 48, 32, 8
+    cam = rt.final_camera(W / H)
+    final_renderer.render(cam, W, H, S, 50, SEED)
+    assert final_renderer.last_segments() == O.fast_segments(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)

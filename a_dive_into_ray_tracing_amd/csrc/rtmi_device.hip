@@ -37,349 +37,39 @@
 #include <vector>
 
 #include "rtmi_internal.h"
+#include "rtmi_path.h"
+
 
 namespace rtmi {
-
-// ---------------------------------------------------------------------------
-// numeric policy
-// ---------------------------------------------------------------------------
-template <class R> struct V3 { R x, y, z; };
-template <class R> __host__ __device__ __forceinline__ V3<R> mk(R x, R y, R z) { return V3<R>{x, y, z}; }
-
-template <bool F> __device__ __forceinline__ float madd(float a, float b, float c) {
-  if constexpr (F) return __builtin_fmaf(a, b, c);
-  else return a * b + c;
-}
-template <bool F> __device__ __forceinline__ double madd(double a, double b, double c) {
-  if constexpr (F) return __builtin_fma(a, b, c);
-  else return a * b + c;
-}
-__device__ __forceinline__ float dsqrt(float x) { return __builtin_sqrtf(x); }
-__device__ __forceinline__ double dsqrt(double x) { return __builtin_sqrt(x); }
-__device__ __forceinline__ float dfabs(float x) { return __builtin_fabsf(x); }
-__device__ __forceinline__ double dfabs(double x) { return __builtin_fabs(x); }
-__device__ __forceinline__ float dfmin(float a, float b) { return __builtin_fminf(a, b); }
-__device__ __forceinline__ double dfmin(double a, double b) { return __builtin_fmin(a, b); }
-// pow((1-cosine), 5) material.h:95: the exact path uses the library pow; the
-// fast path multiplies (x^2)^2 * x (the CPU restatement does the same).
-__device__ __forceinline__ float pow5(float x) { float x2 = x * x; float x4 = x2 * x2; return x4 * x; }
-__device__ __forceinline__ double pow5(double x) { return pow(x, 5.0); }
-
-// dot vec3.h:77-79
-template <bool F, class R> __device__ __forceinline__ R dot(V3<R> a, V3<R> b) {
-  return madd<F>(a.z, b.z, madd<F>(a.y, b.y, a.x * b.x));
-}
-template <class R> __device__ __forceinline__ V3<R> scale(R t, V3<R> v) { return mk(t * v.x, t * v.y, t * v.z); }
-// unit_vector vec3.h:101 (operator/ is (1/t)*v, vec3.h:89)
-template <bool F, class R> __device__ __forceinline__ V3<R> unit(V3<R> v) {
-  return scale(R(1) / dsqrt(dot<F>(v, v)), v);
-}
-// reflect vec3.h:114
-template <bool F, class R> __device__ __forceinline__ V3<R> reflect(V3<R> v, V3<R> n) {
-  const R k = R(2) * dot<F>(v, n);
-  return mk(madd<F>(-k, n.x, v.x), madd<F>(-k, n.y, v.y), madd<F>(-k, n.z, v.z));
-}
-// refract vec3.h:116-121 (cos_theta identical to the caller's, material.h:72)
-template <bool F, class R> __device__ __forceinline__ V3<R> refract(V3<R> uv, V3<R> n, R eta, R cos_theta) {
-  V3<R> perp = mk(eta * madd<F>(cos_theta, n.x, uv.x), eta * madd<F>(cos_theta, n.y, uv.y),
-                  eta * madd<F>(cos_theta, n.z, uv.z));
-  const R s = dsqrt(dfabs(R(1) - dot<F>(perp, perp)));
-  return mk(madd<F>(-s, n.x, perp.x), madd<F>(-s, n.y, perp.y), madd<F>(-s, n.z, perp.z));
-}
-// dielectric::reflectance material.h:91-96 (Schlick)
-template <bool F, class R> __device__ __forceinline__ R reflectance(R cosine, R ref_idx) {
-  R r0 = (R(1) - ref_idx) / (R(1) + ref_idx);
-  r0 = r0 * r0;
-  return madd<F>(R(1) - r0, pow5(R(1) - cosine), r0);
-}
-// near_zero vec3.h:53-57 — keeps the reference's fabs(e[0] < s) slip
-template <class R> __device__ __forceinline__ bool near_zero(V3<R> v) {
-  const R s = R(1e-8);
-  return (v.x < s) && (dfabs(v.y) < s) && (dfabs(v.z) < s);
-}
-
-// ---------------------------------------------------------------------------
-// RNG
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
-  return z ^ (z >> 31);
-}
-// xoroshiro128+ (a=24, b=16, c=37), state from splitmix64 finalisers of the
-// key (seed, pixel, sample): a counter-based stream per camera sample.
-struct Xoro {
-  uint64_t s0, s1;
-  __device__ __forceinline__ void init(uint64_t seed, uint64_t pixel, uint32_t sample) {
-    const uint64_t key = (pixel << 24) | uint64_t(sample);
-    s0 = mix64(seed ^ mix64(key + 0x9E3779B97F4A7C15ULL));
-    s1 = mix64(s0 + 0x9E3779B97F4A7C15ULL);
-  }
-  __device__ __forceinline__ uint64_t next() {
-    const uint64_t a = s0, r = s0 + s1;
-    uint64_t b = s1 ^ a;
-    s0 = ((a << 24) | (a >> 40)) ^ b ^ (b << 16);
-    s1 = (b << 37) | (b >> 27);
-    return r;
-  }
-  // top 24 bits: uniform on [0,1) exactly representable in float
-  __device__ __forceinline__ float uni() { return float(uint32_t(next() >> 40)) * 0x1p-24f; }
-};
-
-// Replays a supplied glibc rand() stream: random_double() = rand()/(RAND_MAX+1.0)
-struct StreamRng {
-  const int32_t *p;
-  int64_t pos, end;
-  bool overflow;
-  __device__ __forceinline__ double uni() {
-    if (pos < end) return double(p[pos++]) / 2147483648.0;
-    overflow = true;
-    return 0.5;
-  }
-};
-
-// random_double(-1,1) rtweekend.h:26-29: min + (max-min)*rd()
-template <class R, class G> __device__ __forceinline__ R rd_m11(G &g) { return R(-1) + R(2) * R(g.uni()); }
-// random_in_unit_sphere vec3.h:103-110: vec3::random(-1,1) draws z, y, x (GCC)
-template <bool F, class R, class G> __device__ __forceinline__ V3<R> in_sphere(G &g) {
-  for (;;) {
-    const R z = rd_m11<R>(g);
-    const R y = rd_m11<R>(g);
-    const R x = rd_m11<R>(g);
-    const V3<R> p = mk(x, y, z);
-    if (dot<F>(p, p) >= R(1)) continue;
-    return p;
-  }
-}
-// random_in_unit_disk vec3.h:123-130: draws y, x (GCC)
-template <bool F, class R, class G> __device__ __forceinline__ V3<R> in_disk(G &g) {
-  for (;;) {
-    const R y = rd_m11<R>(g);
-    const R x = rd_m11<R>(g);
-    if (madd<F>(y, y, x * x) >= R(1)) continue;
-    return mk(x, y, R(0));
-  }
-}
-
-// ---------------------------------------------------------------------------
-// scene / camera views
-// ---------------------------------------------------------------------------
-template <class R> struct V4T;
-template <> struct V4T<float> { using type = float4; };
-template <> struct V4T<double> { using type = double4; };
-
-// geom[k]  = {cx, cy, cz, r*r}
-// shade0[k] = {1/r, albedo r, g, b}
-// shade1[k] = {kind, fuzz (clamped), ir, 1/ir}
-template <class R> struct SceneView {
-  const typename V4T<R>::type *__restrict__ geom;
-  const typename V4T<R>::type *__restrict__ sh0;
-  const typename V4T<R>::type *__restrict__ sh1;
-  int32_t n;
-};
-
-template <class R> struct Cam {
-  V3<R> origin, llc, hor, ver, u, v;
-  R lens;
-};
-
-// camera::get_ray camera.h:56-62
-template <bool F, class R, class G>
-__device__ __forceinline__ void get_ray(const Cam<R> &c, R s, R t, G &g, V3<R> &o, V3<R> &d) {
-  const V3<R> p = in_disk<F, R>(g);
-  const R rdx = c.lens * p.x, rdy = c.lens * p.y;
-  const V3<R> off = mk(madd<F>(rdy, c.v.x, rdx * c.u.x), madd<F>(rdy, c.v.y, rdx * c.u.y),
-                       madd<F>(rdy, c.v.z, rdx * c.u.z));
-  o = mk(c.origin.x + off.x, c.origin.y + off.y, c.origin.z + off.z);
-  d = mk((madd<F>(t, c.ver.x, madd<F>(s, c.hor.x, c.llc.x)) - c.origin.x) - off.x,
-         (madd<F>(t, c.ver.y, madd<F>(s, c.hor.y, c.llc.y)) - c.origin.y) - off.y,
-         (madd<F>(t, c.ver.z, madd<F>(s, c.hor.z, c.llc.z)) - c.origin.z) - off.z);
-}
-
-// hittable_list::hit over sphere::hit: closest root in the closed interval
-// [t_min, closest_so_far]; ties go to the later object (sphere.h:36-41).
-// The (hb >= 0 && cc >= 0) skip never changes the result: both roots are
-// <= 0 < t_min there.  In the fast path the wave runs this
-// loop in lockstep with sphere k in SGPRs.
-template <bool F, class R>
-__device__ __forceinline__ int32_t hit_world(const SceneView<R> &sc, V3<R> o, V3<R> d, R &t_hit) {
-  const R a = dot<F>(d, d);
-  const R inv_a = R(1) / a;
-  const R t_min = R(0.001);
-  R t_max = R(INFINITY);
-  int32_t best = -1;
-#pragma unroll 4
-  for (int32_t k = 0; k < sc.n; ++k) {
-    const auto s = sc.geom[k];
-    const R ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;
-    const R hb = madd<F>(ocz, d.z, madd<F>(ocy, d.y, ocx * d.x));
-    const R cc = madd<F>(ocz, ocz, madd<F>(ocy, ocy, ocx * ocx)) - s.w;
-    const R disc = madd<F>(hb, hb, -(a * cc));
-    if (!(disc < R(0)) && !(hb >= R(0) && cc >= R(0))) {
-      const R sq = dsqrt(disc);
-      R root = F ? (-hb - sq) * inv_a : (-hb - sq) / a;
-      bool ok = !(root < t_min || t_max < root);
-      if (!ok) {
-        root = F ? (-hb + sq) * inv_a : (-hb + sq) / a;
-        ok = !(root < t_min || t_max < root);
-      }
-      if (ok) {
-        t_max = root;
-        best = k;
-      }
-    }
-  }
-  t_hit = t_max;
-  return best;
-}
-
-// The fast path's form of hit_world: spheres in groups of G.  The group's
-// {centre, r^2} are wave-uniform scalar loads (s_load_dwordx16 for G = 4),
-// the G discriminants are computed branch-free (independent chains), and the
-// wave takes ONE branch per group when no lane has a candidate — the common
-// case.  The candidate test is the sign-bit form of
-//     !(disc < 0) && !(hb >= 0 && cc >= 0)
-// (skips a subset of what that skips, so every skip stays result-preserving,
-// DESIGN.md §3.2).  Candidates are resolved in sphere order, so ties and the
-// shrinking t_max behave exactly as the sequential loop of hit_world above.
-template <int G>
-__device__ __forceinline__ int32_t hit_world_grouped(const float4 *__restrict__ geom, int32_t n, V3<float> o,
-                                                     V3<float> d, float &t_hit) {
-  const float a = dot<true>(d, d);
-  const float na = -a;  // na*cc == -(a*cc) exactly: saves the negation per sphere
-  const float inv_a = 1.0f / a;
-  const float t_min = 0.001f;
-  float t_max = INFINITY;
-  int32_t best = -1;
-  auto resolve = [&](int32_t idx, float hb, float disc) {
-    const float sq = dsqrt(disc);
-    float root = (-hb - sq) * inv_a;
-    bool ok = !(root < t_min || t_max < root);
-    if (!ok) {
-      root = (-hb + sq) * inv_a;
-      ok = !(root < t_min || t_max < root);
-    }
-    if (ok) {
-      t_max = root;
-      best = idx;
-    }
-  };
-  auto test = [&](const float4 s, float &hb, float &disc) -> int {
-    const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;
-    hb = __builtin_fmaf(ocz, d.z, __builtin_fmaf(ocy, d.y, ocx * d.x));
-    const float cc = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - s.w;
-    disc = __builtin_fmaf(hb, hb, na * cc);
-    return (__float_as_int(hb) | __float_as_int(cc)) & ~__float_as_int(disc);  // < 0: candidate
-  };
-  int32_t k = 0;
-  for (; k + G <= n; k += G) {
-    float4 s[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) s[g] = geom[k + g];
-    float hb[G], disc[G];
-    int ci[G];
-    int any = 0;
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      ci[g] = test(s[g], hb[g], disc[g]);
-      any |= ci[g];
-    }
-    if (any < 0) {
-#pragma unroll
-      for (int g = 0; g < G; ++g)
-        if (ci[g] < 0) resolve(k + g, hb[g], disc[g]);
-    }
-  }
-  for (; k < n; ++k) {
-    float hb, disc;
-    if (test(geom[k], hb, disc) < 0) resolve(k, hb, disc);
-  }
-  t_hit = t_max;
-  return best;
-}
-
-// material::scatter material.h:15-97.  Returns true if the ray scattered.
-template <bool F, class R, class G>
-__device__ __forceinline__ bool scatter(const SceneView<R> &sc, int32_t k, V3<R> din, V3<R> normal,
-                                        bool front, G &g, V3<R> &atten, V3<R> &dout) {
-  const auto s0 = sc.sh0[k];
-  const auto s1 = sc.sh1[k];
-  const int kind = int(s1.x);
-  if (kind == RT_MAT_LAMBERTIAN) {  // material.h:19-31
-    const V3<R> ru = unit<F>(in_sphere<F, R>(g));
-    V3<R> dir = mk(normal.x + ru.x, normal.y + ru.y, normal.z + ru.z);
-    if (near_zero(dir)) dir = normal;
-    dout = dir;
-    atten = mk(s0.y, s0.z, s0.w);
-    return true;
-  }
-  if (kind == RT_MAT_METAL) {  // material.h:40-49
-    const V3<R> refl = reflect<F>(unit<F>(din), normal);
-    const V3<R> rv = in_sphere<F, R>(g);
-    const R fz = s1.y;
-    const V3<R> dir = mk(madd<F>(fz, rv.x, refl.x), madd<F>(fz, rv.y, refl.y), madd<F>(fz, rv.z, refl.z));
-    dout = dir;
-    atten = mk(s0.y, s0.z, s0.w);
-    return dot<F>(dir, normal) > R(0);
-  }
-  // dielectric material.h:60-85
-  atten = mk(R(1), R(1), R(1));
-  const R ratio = front ? s1.w : s1.z;
-  const V3<R> ud = unit<F>(din);
-  const R cos_theta = dfmin(dot<F>(mk(-ud.x, -ud.y, -ud.z), normal), R(1));
-  const R sin_theta = dsqrt(madd<F>(-cos_theta, cos_theta, R(1)));
-  const bool cannot_refract = ratio * sin_theta > R(1);
-  if (cannot_refract || reflectance<F>(cos_theta, ratio) > R(g.uni()))
-    dout = reflect<F>(ud, normal);
-  else
-    dout = refract<F>(ud, normal, ratio, cos_theta);
-  return true;
-}
-
-// Hit record (sphere.h:43-53, hittable.h:23-26) for sphere k at t.
-template <bool F, class R>
-__device__ __forceinline__ void hit_record(const SceneView<R> &sc, int32_t k, V3<R> o, V3<R> d, R t,
-                                           V3<R> &p, V3<R> &normal, bool &front) {
-  const auto g = sc.geom[k];
-  const R inv_r = sc.sh0[k].x;
-  p = mk(madd<F>(t, d.x, o.x), madd<F>(t, d.y, o.y), madd<F>(t, d.z, o.z));  // ray::at ray.h:15
-  const V3<R> outward = scale(inv_r, mk(p.x - g.x, p.y - g.y, p.z - g.z));
-  front = dot<F>(d, outward) < R(0);
-  normal = front ? outward : mk(-outward.x, -outward.y, -outward.z);
-}
-
-// sky, main.cpp:80-82
-template <bool F, class R> __device__ __forceinline__ V3<R> sky(V3<R> d) {
-  const R uy = (R(1) / dsqrt(dot<F>(d, d))) * d.y;
-  const R t = R(0.5) * (uy + R(1));
-  return mk(madd<F>(t, R(0.5), R(1) - t), madd<F>(t, R(0.7), R(1) - t), madd<F>(t, R(1), R(1) - t));
-}
 
 // ---------------------------------------------------------------------------
 // fast render kernel
 // ---------------------------------------------------------------------------
 struct RenderArgs {
   Cam<float> cam;
-  int32_t n, W, H, spp, max_depth;
+  int32_t n, npairs, W, H, spp, max_depth;
   uint64_t seed;
   int32_t row0, row_step, nrows_valid;
   int32_t tiles_x, chunk, n_chunks, n_items;
 };
 
 constexpr int kWavesPerBlock = 4;
-#ifndef RTMI_SPHERE_GROUP
-#define RTMI_SPHERE_GROUP 4
+#ifndef RTMI_WAVES_PER_EU
+#define RTMI_WAVES_PER_EU 1
 #endif
-constexpr int kSphereGroup = RTMI_SPHERE_GROUP;
+#ifndef RTMI_PAIR_GROUP
+#define RTMI_PAIR_GROUP 4
+#endif
+constexpr int kPairGroup = RTMI_PAIR_GROUP;  // sphere pairs per scalar-load group
 
 __device__ __forceinline__ int64_t to_fixed(float c) { return int64_t(c * 4294967296.0f); }
 __device__ __forceinline__ float from_fixed(int64_t v) { return float(v) * 0x1p-32f; }
 
 template <int TW, bool CHUNKED>
-__global__ __launch_bounds__(64 * kWavesPerBlock) void render_kernel(
+__global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render_kernel(
     const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1,
-    RenderArgs a, unsigned long long *__restrict__ accum, float *__restrict__ out,
-    unsigned long long *__restrict__ segments) {
+    const SpherePair *__restrict__ pairs, RenderArgs a, unsigned long long *__restrict__ accum,
+    float *__restrict__ out, unsigned long long *__restrict__ segments) {
   constexpr int TH = 64 / TW;
   __shared__ unsigned long long acc[kWavesPerBlock][3][64];
   __shared__ unsigned long long wave_segs[kWavesPerBlock];
@@ -403,6 +93,9 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void render_kernel(
   acc[wave][2][lane] = 0;
   if (lane == 0) wave_segs[wave] = 0;
   unsigned nseg = 0;  // world.hit calls of this lane (algorithmic-work accounting)
+#if RTMI_STATS
+  unsigned stats[3] = {0, 0, 0};  // groups, groups with a candidate (wave), resolves (lane)
+#endif
 
   const SceneView<float> sc{geom, sh0, sh1, a.n};
   const float inv_wm1 = 0.f;  // (unused; divisions below follow main.cpp:278-279)
@@ -439,7 +132,11 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void render_kernel(
     if (active) {
       float t;
       ++nseg;
-      const int k = hit_world_grouped<kSphereGroup>(geom, a.n, o, d, t);
+      const int k = hit_world_packed<kPairGroup>(pairs, a.npairs, o, d, t
+#if RTMI_STATS
+                                                 , stats
+#endif
+      );
       if (k < 0) {
         const V3<float> sk = sky<true, float>(d);
         col = mk(T.x * sk.x, T.y * sk.y, T.z * sk.z);
@@ -486,6 +183,10 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void render_kernel(
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   if (lane == 0) atomicAdd(segments, wave_segs[wave]);
+#if RTMI_STATS
+  if (lane == 0) { atomicAdd(&segments[1], (unsigned long long)stats[0]); atomicAdd(&segments[2], (unsigned long long)stats[1]); }
+  atomicAdd(&segments[3], (unsigned long long)stats[2]);
+#endif
   if (lane < nv) {
     const int ly = lane / vw, lx = lane - ly * vw;
     const size_t o3 = (size_t(y0 + ly) * size_t(a.W) + size_t(x0 + lx)) * 3;
@@ -585,6 +286,8 @@ struct rt_ctx {
   hipStream_t stream = nullptr;
   int32_t n = 0;
   float4 *geom = nullptr, *sh0 = nullptr, *sh1 = nullptr;
+  SpherePair *pairs = nullptr;
+  int32_t npairs = 0;
   double4 *geom64 = nullptr, *sh064 = nullptr, *sh164 = nullptr;
   unsigned long long *accum = nullptr;
   size_t accum_cap = 0;  // elements
@@ -671,8 +374,8 @@ RTMI_EXPORT int rt_ctx_create(int32_t device, rt_ctx **out) {
   auto ctx = std::make_unique<rt_ctx>();
   ctx->device = device;
   HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-  if (int rc = dev_alloc(&ctx->segments, 1)) return rc;
-  HIP_TRY(hipMemset(ctx->segments, 0, sizeof(unsigned long long)));
+  if (int rc = dev_alloc(&ctx->segments, 4)) return rc;
+  HIP_TRY(hipMemset(ctx->segments, 0, 4 * sizeof(unsigned long long)));
   *out = ctx.release();
   return RT_OK;
 }
@@ -682,7 +385,7 @@ RTMI_EXPORT int rt_ctx_destroy(rt_ctx *ctx) {
   DeviceGuard guard(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   for (void *p : {(void *)ctx->geom, (void *)ctx->sh0, (void *)ctx->sh1, (void *)ctx->geom64, (void *)ctx->sh064,
-                  (void *)ctx->sh164, (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments})
+                  (void *)ctx->sh164, (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments, (void *)ctx->pairs})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -693,7 +396,7 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
   if (!ctx || !scene || scene->n <= 0 || !scene->center_radius || !scene->mat_kind || !scene->mat_params)
     return set_error(RT_EINVAL, "rt_ctx_set_scene: bad argument");
   const int n = scene->n;
-  std::vector<float4> g(n), s0(n), s1(n);
+  std::vector<float4> g(n + kGeomPad, make_float4(0.f, 0.f, 0.f, 0.f)), s0(n), s1(n);
   std::vector<double4> g64(n), s064(n), s164(n);
   for (int k = 0; k < n; k++) {
     const double *c = scene->center_radius + 4 * k;
@@ -703,20 +406,40 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
       return set_error(RT_EUNSUPPORTED, "object %d: unsupported material kind %d", k, kind);
     const double fuzz = m[3] < 1 ? m[3] : 1;  // metal ctor material.h:39
     const float r = float(c[3]), ir = float(m[3]);
-    g[k] = make_float4(float(c[0]), float(c[1]), float(c[2]), r * r);
+    // S = |c|^2 - r^2 of the float-rounded sphere, in double then rounded
+    // (the oracle computes the identical expression)
+    const float cx = float(c[0]), cy = float(c[1]), cz = float(c[2]);
+    const float S = float(double(cx) * cx + double(cy) * cy + double(cz) * cz - double(r) * r);
+    g[k] = make_float4(cx, cy, cz, S);
     s0[k] = make_float4(1.0f / r, float(m[0]), float(m[1]), float(m[2]));
     s1[k] = make_float4(float(kind), float(fuzz), ir, 1.0f / ir);
     g64[k] = make_double4(c[0], c[1], c[2], c[3] * c[3]);
     s064[k] = make_double4(1 / c[3], m[0], m[1], m[2]);
     s164[k] = make_double4(double(kind), fuzz, m[3], 1.0 / m[3]);
   }
+  // sphere pairs for the packed loop: n padded to a multiple of 2*kPairGroup
+  // with never-hit dummies, plus kPairGroup pairs of prefetch padding
+  const int n_pad = (n + 2 * kPairGroup - 1) / (2 * kPairGroup) * (2 * kPairGroup);
+  const int npairs = n_pad / 2;
+  std::vector<SpherePair> pr(npairs + kPairGroup);
+  for (auto &p : pr) {
+    p.cx = f2v{0.f, 0.f}; p.cy = f2v{0.f, 0.f}; p.cz = f2v{0.f, 0.f}; p.S = f2v{kDummyS, kDummyS};
+  }
+  for (int k = 0; k < n; k++) {
+    SpherePair &p = pr[k / 2];
+    const int h = k & 1;
+    p.cx[h] = g[k].x; p.cy[h] = g[k].y; p.cz[h] = g[k].z; p.S[h] = g[k].w;
+  }
   DeviceGuard guard(ctx->device);
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   int rc;
-  if ((rc = dev_alloc(&ctx->geom, n)) || (rc = dev_alloc(&ctx->sh0, n)) || (rc = dev_alloc(&ctx->sh1, n)) ||
-      (rc = dev_alloc(&ctx->geom64, n)) || (rc = dev_alloc(&ctx->sh064, n)) || (rc = dev_alloc(&ctx->sh164, n)))
+  if ((rc = dev_alloc(&ctx->geom, n + kGeomPad)) || (rc = dev_alloc(&ctx->sh0, n)) || (rc = dev_alloc(&ctx->sh1, n)) ||
+      (rc = dev_alloc(&ctx->geom64, n)) || (rc = dev_alloc(&ctx->sh064, n)) || (rc = dev_alloc(&ctx->sh164, n)) ||
+      (rc = dev_alloc(&ctx->pairs, pr.size())))
     return rc;
-  HIP_TRY(hipMemcpy(ctx->geom, g.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(ctx->pairs, pr.data(), pr.size() * sizeof(SpherePair), hipMemcpyHostToDevice));
+  ctx->npairs = npairs;
+  HIP_TRY(hipMemcpy(ctx->geom, g.data(), (n + kGeomPad) * sizeof(float4), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(ctx->sh0, s0.data(), n * sizeof(float4), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(ctx->sh1, s1.data(), n * sizeof(float4), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(ctx->geom64, g64.data(), n * sizeof(double4), hipMemcpyHostToDevice));
@@ -743,10 +466,10 @@ void launch_tw(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const
                unsigned long long *accum, float *out) {
   if (chunked)
     hipLaunchKernelGGL((render_kernel<TW, true>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
-                       ctx->sh1, a, accum, out, ctx->segments);
+                       ctx->sh1, ctx->pairs, a, accum, out, ctx->segments);
   else
     hipLaunchKernelGGL((render_kernel<TW, false>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
-                       ctx->sh1, a, accum, out, ctx->segments);
+                       ctx->sh1, ctx->pairs, a, accum, out, ctx->segments);
 }
 
 // The render of one row set into a device strip; all work on `st`.
@@ -754,7 +477,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
                      uint64_t seed, int32_t row0, int32_t row_step, int32_t nrows, float *strip, hipStream_t st) {
   const size_t n_out = size_t(nrows) * size_t(W) * 3;
   ctx->last_stream = st;
-  HIP_TRY(hipMemsetAsync(ctx->segments, 0, sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(ctx->segments, 0, 4 * sizeof(unsigned long long), st));
   if (nrows == 0) return RT_OK;
   // valid rows: row0 + r*row_step < H
   int32_t nvalid = 0;
@@ -787,6 +510,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   RenderArgs a;
   a.cam = cam_f(cam);
   a.n = ctx->n;
+  a.npairs = ctx->npairs;
   a.W = W; a.H = H; a.spp = spp; a.max_depth = max_depth; a.seed = seed;
   a.row0 = row0; a.row_step = row_step; a.nrows_valid = nvalid;
   a.tiles_x = tiles_x; a.chunk = chunk; a.n_chunks = n_chunks; a.n_items = int32_t(items);
@@ -917,5 +641,19 @@ RTMI_EXPORT int rt_ctx_last_segments(rt_ctx *ctx, uint64_t *segments) {
   HIP_TRY(hipMemcpyAsync(&v, ctx->segments, sizeof v, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   *segments = v;
+  return RT_OK;
+}
+
+// Debug counters of the last render (RTMI_STATS builds only; zeros otherwise):
+// out[0] = world.hit calls, out[1] = sphere groups tested (per wave),
+// out[2] = groups where some lane had a candidate, out[3] = candidate resolves.
+RTMI_EXPORT int rt_ctx_debug_counters(rt_ctx *ctx, uint64_t *out) {
+  if (!ctx || !out) return set_error(RT_EINVAL, "null argument");
+  DeviceGuard guard(ctx->device);
+  hipStream_t st = ctx->last_stream ? ctx->last_stream : ctx->stream;
+  unsigned long long v[4] = {0, 0, 0, 0};
+  HIP_TRY(hipMemcpyAsync(v, ctx->segments, sizeof v, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  for (int i = 0; i < 4; i++) out[i] = v[i];
   return RT_OK;
 }

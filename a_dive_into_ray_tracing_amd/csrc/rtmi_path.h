@@ -1,0 +1,570 @@
+// rtmi_path.h — device-side path tracing for librtmi: numeric policy, RNG,
+// camera ray, ray-sphere loops, materials (the reference's L0-L4 layers:
+// vec3.h, ray.h, camera.h, sphere.h, hittable_list.h, material.h,
+// main.cpp:57-83).  Included by rtmi_device.hip (the kernels) and by
+// tools/loopbench.hip (the sphere-loop microbenchmark).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "../../include/rtmi.h"
+
+#ifndef RTMI_PREFETCH
+#define RTMI_PREFETCH 0
+#endif
+#ifndef RTMI_STATS
+#define RTMI_STATS 0
+#endif
+#ifndef RTMI_DISC_ONLY
+#define RTMI_DISC_ONLY 1
+#endif
+
+namespace rtmi {
+
+
+constexpr int kGeomPad = 16;  // zero spheres after the scene: prefetch reads past n stay in bounds
+
+// ---------------------------------------------------------------------------
+// numeric policy
+// ---------------------------------------------------------------------------
+template <class R> struct V3 { R x, y, z; };
+template <class R> __host__ __device__ __forceinline__ V3<R> mk(R x, R y, R z) { return V3<R>{x, y, z}; }
+
+template <bool F> __device__ __forceinline__ float madd(float a, float b, float c) {
+  if constexpr (F) return __builtin_fmaf(a, b, c);
+  else return a * b + c;
+}
+template <bool F> __device__ __forceinline__ double madd(double a, double b, double c) {
+  if constexpr (F) return __builtin_fma(a, b, c);
+  else return a * b + c;
+}
+__device__ __forceinline__ float dsqrt(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ double dsqrt(double x) { return __builtin_sqrt(x); }
+__device__ __forceinline__ float dfabs(float x) { return __builtin_fabsf(x); }
+__device__ __forceinline__ double dfabs(double x) { return __builtin_fabs(x); }
+__device__ __forceinline__ float dfmin(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ double dfmin(double a, double b) { return __builtin_fmin(a, b); }
+// pow((1-cosine), 5) material.h:95: the exact path uses the library pow; the
+// fast path multiplies (x^2)^2 * x (the CPU restatement does the same).
+__device__ __forceinline__ float pow5(float x) { float x2 = x * x; float x4 = x2 * x2; return x4 * x; }
+__device__ __forceinline__ double pow5(double x) { return pow(x, 5.0); }
+
+// dot vec3.h:77-79
+template <bool F, class R> __device__ __forceinline__ R dot(V3<R> a, V3<R> b) {
+  return madd<F>(a.z, b.z, madd<F>(a.y, b.y, a.x * b.x));
+}
+template <class R> __device__ __forceinline__ V3<R> scale(R t, V3<R> v) { return mk(t * v.x, t * v.y, t * v.z); }
+// unit_vector vec3.h:101 (operator/ is (1/t)*v, vec3.h:89)
+template <bool F, class R> __device__ __forceinline__ V3<R> unit(V3<R> v) {
+  return scale(R(1) / dsqrt(dot<F>(v, v)), v);
+}
+// reflect vec3.h:114
+template <bool F, class R> __device__ __forceinline__ V3<R> reflect(V3<R> v, V3<R> n) {
+  const R k = R(2) * dot<F>(v, n);
+  return mk(madd<F>(-k, n.x, v.x), madd<F>(-k, n.y, v.y), madd<F>(-k, n.z, v.z));
+}
+// refract vec3.h:116-121 (cos_theta identical to the caller's, material.h:72)
+template <bool F, class R> __device__ __forceinline__ V3<R> refract(V3<R> uv, V3<R> n, R eta, R cos_theta) {
+  V3<R> perp = mk(eta * madd<F>(cos_theta, n.x, uv.x), eta * madd<F>(cos_theta, n.y, uv.y),
+                  eta * madd<F>(cos_theta, n.z, uv.z));
+  const R s = dsqrt(dfabs(R(1) - dot<F>(perp, perp)));
+  return mk(madd<F>(-s, n.x, perp.x), madd<F>(-s, n.y, perp.y), madd<F>(-s, n.z, perp.z));
+}
+// dielectric::reflectance material.h:91-96 (Schlick)
+template <bool F, class R> __device__ __forceinline__ R reflectance(R cosine, R ref_idx) {
+  R r0 = (R(1) - ref_idx) / (R(1) + ref_idx);
+  r0 = r0 * r0;
+  return madd<F>(R(1) - r0, pow5(R(1) - cosine), r0);
+}
+// near_zero vec3.h:53-57 — keeps the reference's fabs(e[0] < s) slip
+template <class R> __device__ __forceinline__ bool near_zero(V3<R> v) {
+  const R s = R(1e-8);
+  return (v.x < s) && (dfabs(v.y) < s) && (dfabs(v.z) < s);
+}
+
+// ---------------------------------------------------------------------------
+// RNG
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+// xoroshiro128+ (a=24, b=16, c=37), state from splitmix64 finalisers of the
+// key (seed, pixel, sample): a counter-based stream per camera sample.
+struct Xoro {
+  uint64_t s0, s1;
+  __device__ __forceinline__ void init(uint64_t seed, uint64_t pixel, uint32_t sample) {
+    const uint64_t key = (pixel << 24) | uint64_t(sample);
+    s0 = mix64(seed ^ mix64(key + 0x9E3779B97F4A7C15ULL));
+    s1 = mix64(s0 + 0x9E3779B97F4A7C15ULL);
+  }
+  __device__ __forceinline__ uint64_t next() {
+    const uint64_t a = s0, r = s0 + s1;
+    uint64_t b = s1 ^ a;
+    s0 = ((a << 24) | (a >> 40)) ^ b ^ (b << 16);
+    s1 = (b << 37) | (b >> 27);
+    return r;
+  }
+  // top 24 bits: uniform on [0,1) exactly representable in float
+  __device__ __forceinline__ float uni() { return float(uint32_t(next() >> 40)) * 0x1p-24f; }
+};
+
+// Replays a supplied glibc rand() stream: random_double() = rand()/(RAND_MAX+1.0)
+struct StreamRng {
+  const int32_t *p;
+  int64_t pos, end;
+  bool overflow;
+  __device__ __forceinline__ double uni() {
+    if (pos < end) return double(p[pos++]) / 2147483648.0;
+    overflow = true;
+    return 0.5;
+  }
+};
+
+// random_double(-1,1) rtweekend.h:26-29: min + (max-min)*rd()
+template <class R, class G> __device__ __forceinline__ R rd_m11(G &g) { return R(-1) + R(2) * R(g.uni()); }
+// random_in_unit_sphere vec3.h:103-110: vec3::random(-1,1) draws z, y, x (GCC)
+template <bool F, class R, class G> __device__ __forceinline__ V3<R> in_sphere(G &g) {
+  for (;;) {
+    const R z = rd_m11<R>(g);
+    const R y = rd_m11<R>(g);
+    const R x = rd_m11<R>(g);
+    const V3<R> p = mk(x, y, z);
+    if (dot<F>(p, p) >= R(1)) continue;
+    return p;
+  }
+}
+// random_in_unit_disk vec3.h:123-130: draws y, x (GCC)
+template <bool F, class R, class G> __device__ __forceinline__ V3<R> in_disk(G &g) {
+  for (;;) {
+    const R y = rd_m11<R>(g);
+    const R x = rd_m11<R>(g);
+    if (madd<F>(y, y, x * x) >= R(1)) continue;
+    return mk(x, y, R(0));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// scene / camera views
+// ---------------------------------------------------------------------------
+template <class R> struct V4T;
+template <> struct V4T<float> { using type = float4; };
+template <> struct V4T<double> { using type = double4; };
+
+// geom[k]  = {cx, cy, cz, |c|^2 - r^2} (float path) / {cx, cy, cz, r*r} (double path)
+// shade0[k] = {1/r, albedo r, g, b}
+// shade1[k] = {kind, fuzz (clamped), ir, 1/ir}
+template <class R> struct SceneView {
+  const typename V4T<R>::type *__restrict__ geom;
+  const typename V4T<R>::type *__restrict__ sh0;
+  const typename V4T<R>::type *__restrict__ sh1;
+  int32_t n;
+};
+
+template <class R> struct Cam {
+  V3<R> origin, llc, hor, ver, u, v;
+  R lens;
+};
+
+// camera::get_ray camera.h:56-62
+template <bool F, class R, class G>
+__device__ __forceinline__ void get_ray(const Cam<R> &c, R s, R t, G &g, V3<R> &o, V3<R> &d) {
+  const V3<R> p = in_disk<F, R>(g);
+  const R rdx = c.lens * p.x, rdy = c.lens * p.y;
+  const V3<R> off = mk(madd<F>(rdy, c.v.x, rdx * c.u.x), madd<F>(rdy, c.v.y, rdx * c.u.y),
+                       madd<F>(rdy, c.v.z, rdx * c.u.z));
+  o = mk(c.origin.x + off.x, c.origin.y + off.y, c.origin.z + off.z);
+  d = mk((madd<F>(t, c.ver.x, madd<F>(s, c.hor.x, c.llc.x)) - c.origin.x) - off.x,
+         (madd<F>(t, c.ver.y, madd<F>(s, c.hor.y, c.llc.y)) - c.origin.y) - off.y,
+         (madd<F>(t, c.ver.z, madd<F>(s, c.hor.z, c.llc.z)) - c.origin.z) - off.z);
+}
+
+// hittable_list::hit over sphere::hit: closest root in the closed interval
+// [t_min, closest_so_far]; ties go to the later object (sphere.h:36-41).
+// The (hb >= 0 && cc >= 0) skip never changes the result: both roots are
+// <= 0 < t_min there.  In the fast path the wave runs this
+// loop in lockstep with sphere k in SGPRs.
+template <bool F, class R>
+__device__ __forceinline__ int32_t hit_world(const SceneView<R> &sc, V3<R> o, V3<R> d, R &t_hit) {
+  const R a = dot<F>(d, d);
+  const R inv_a = R(1) / a;
+  const R t_min = R(0.001);
+  R t_max = R(INFINITY);
+  int32_t best = -1;
+#pragma unroll 4
+  for (int32_t k = 0; k < sc.n; ++k) {
+    const auto s = sc.geom[k];
+    const R ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;
+    const R hb = madd<F>(ocz, d.z, madd<F>(ocy, d.y, ocx * d.x));
+    const R cc = madd<F>(ocz, ocz, madd<F>(ocy, ocy, ocx * ocx)) - s.w;
+    const R disc = madd<F>(hb, hb, -(a * cc));
+    if (!(disc < R(0)) && !(hb >= R(0) && cc >= R(0))) {
+      const R sq = dsqrt(disc);
+      R root = F ? (-hb - sq) * inv_a : (-hb - sq) / a;
+      bool ok = !(root < t_min || t_max < root);
+      if (!ok) {
+        root = F ? (-hb + sq) * inv_a : (-hb + sq) / a;
+        ok = !(root < t_min || t_max < root);
+      }
+      if (ok) {
+        t_max = root;
+        best = k;
+      }
+    }
+  }
+  t_hit = t_max;
+  return best;
+}
+
+// The fast path's form of hit_world: spheres in groups of G.  The group's
+// {centre, r^2} are wave-uniform scalar loads (s_load_dwordx16 for G = 4),
+// the G discriminants are computed branch-free (independent chains), and the
+// wave takes ONE branch per group when no lane has a candidate — the common
+// case.  The candidate test is the sign-bit form of
+//     !(disc < 0) && !(hb >= 0 && cc >= 0)
+// (skips a subset of what that skips, so every skip stays result-preserving,
+// DESIGN.md §3.2).  Candidates are resolved in sphere order, so ties and the
+// shrinking t_max behave exactly as the sequential loop of hit_world above.
+template <int G>
+__device__ __forceinline__ int32_t hit_world_grouped(const float4 *__restrict__ geom, int32_t n, V3<float> o,
+                                                     V3<float> d, float &t_hit
+#if RTMI_STATS
+                                                     , unsigned *stats
+#endif
+                                                     ) {
+  // Expanded form: per segment K = o.d, aL = a|o|^2,
+  // m2ao = -2a*o; per sphere {c, S = |c|^2 - r^2} in SGPRs:
+  //   hb = K - c.d = (o-c).d,  acc = aL + a*S + m2ao.c = a*(|o-c|^2 - r^2),
+  //   disc = hb*hb - acc
+  // -> 8 FMA-class VALU ops per sphere instead of the literal form's 12.
+  const float a = dot<true>(d, d);
+  const float inv_a = 1.0f / a;
+  const float K = dot<true>(o, d);
+  const float aL = a * dot<true>(o, o);
+  const float n2a = -2.0f * a;
+  const V3<float> m2ao = mk(n2a * o.x, n2a * o.y, n2a * o.z);
+  const float t_min = 0.001f;
+  float t_max = INFINITY;
+  int32_t best = -1;
+  auto resolve = [&](int32_t idx, float hb, float disc) {
+    const float sq = dsqrt(disc);
+    float root = (-hb - sq) * inv_a;
+    bool ok = !(root < t_min || t_max < root);
+    if (!ok) {
+      root = (-hb + sq) * inv_a;
+      ok = !(root < t_min || t_max < root);
+    }
+    if (ok) {
+      t_max = root;
+      best = idx;
+    }
+  };
+  auto test = [&](const float4 s, float &hb, float &disc) -> int {
+    hb = __builtin_fmaf(-s.x, d.x, __builtin_fmaf(-s.y, d.y, __builtin_fmaf(-s.z, d.z, K)));
+    const float acc = __builtin_fmaf(m2ao.x, s.x, __builtin_fmaf(m2ao.y, s.y, __builtin_fmaf(m2ao.z, s.z,
+                                     __builtin_fmaf(a, s.w, aL))));
+    disc = __builtin_fmaf(hb, hb, -acc);
+    return (__float_as_int(hb) | __float_as_int(acc)) & ~__float_as_int(disc);  // < 0: candidate
+  };
+  int32_t k = 0;
+#if RTMI_PREFETCH
+  // software pipeline: group k+G's scalar load is issued before group k is
+  // computed (geom is padded by kGeomPad entries), so its latency hides
+  // behind this group's VALU work instead of stalling the wave.
+  float4 nxt[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) nxt[g] = geom[g];
+#endif
+  for (; k + G <= n; k += G) {
+    float4 s[G];
+#if RTMI_PREFETCH
+#pragma unroll
+    for (int g = 0; g < G; ++g) s[g] = nxt[g];
+#pragma unroll
+    for (int g = 0; g < G; ++g) nxt[g] = geom[k + G + g];
+#else
+#pragma unroll
+    for (int g = 0; g < G; ++g) s[g] = geom[k + g];
+#endif
+    float hb[G], disc[G];
+    int ci[G];
+    int any = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      ci[g] = test(s[g], hb[g], disc[g]);
+      any |= ci[g];
+    }
+#if RTMI_STATS
+    stats[0] += 1;
+    if (__ballot(any < 0)) stats[1] += 1;
+#endif
+    if (any < 0) {
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (ci[g] < 0) {
+#if RTMI_STATS
+          stats[2] += 1;
+#endif
+          resolve(k + g, hb[g], disc[g]);
+        }
+    }
+  }
+  for (; k < n; ++k) {
+    float hb, disc;
+    if (test(geom[k], hb, disc) < 0) resolve(k, hb, disc);
+  }
+  t_hit = t_max;
+  return best;
+}
+
+// Software-pipelined form of hit_world_grouped (experimental, loopbench):
+// two register sets of G spheres; each set's scalar load is issued right
+// after the previous set's first use has forced its s_waitcnt, so a load
+// lands while the other set is computed (SMEM returns out of order, so a
+// wait covers every load outstanding at that point).
+template <int G>
+__device__ __forceinline__ int32_t hit_world_pipelined(const float4 *__restrict__ geom, int32_t n, V3<float> o,
+                                                       V3<float> d, float &t_hit) {
+  const float a = dot<true>(d, d);
+  const float inv_a = 1.0f / a;
+  const float K = dot<true>(o, d);
+  const float aL = a * dot<true>(o, o);
+  const float n2a = -2.0f * a;
+  const V3<float> m2ao = mk(n2a * o.x, n2a * o.y, n2a * o.z);
+  const float t_min = 0.001f;
+  float t_max = INFINITY;
+  int32_t best = -1;
+  auto resolve = [&](int32_t idx, float hb, float disc) {
+    const float sq = dsqrt(disc);
+    float root = (-hb - sq) * inv_a;
+    bool ok = !(root < t_min || t_max < root);
+    if (!ok) {
+      root = (-hb + sq) * inv_a;
+      ok = !(root < t_min || t_max < root);
+    }
+    if (ok) {
+      t_max = root;
+      best = idx;
+    }
+  };
+  auto test = [&](const float4 s, float &hb, float &disc) -> int {
+    hb = __builtin_fmaf(-s.x, d.x, __builtin_fmaf(-s.y, d.y, __builtin_fmaf(-s.z, d.z, K)));
+    const float acc = __builtin_fmaf(m2ao.x, s.x, __builtin_fmaf(m2ao.y, s.y, __builtin_fmaf(m2ao.z, s.z,
+                                     __builtin_fmaf(a, s.w, aL))));
+    disc = __builtin_fmaf(hb, hb, -acc);
+    return (__float_as_int(hb) | __float_as_int(acc)) & ~__float_as_int(disc);
+  };
+  // compute one set; the next set's loads are issued after this set's first
+  // test (which carries the wait for this set)
+  auto group = [&](const float4 (&cur)[G], float4 (&nxt)[G], int32_t k, int32_t knext) {
+    float hb[G], disc[G];
+    int ci[G];
+    ci[0] = test(cur[0], hb[0], disc[0]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 0; g < G; ++g) nxt[g] = geom[knext + g];
+    __builtin_amdgcn_sched_barrier(0);
+    int any = ci[0];
+#pragma unroll
+    for (int g = 1; g < G; ++g) {
+      ci[g] = test(cur[g], hb[g], disc[g]);
+      any |= ci[g];
+    }
+    if (any < 0) {
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (ci[g] < 0) resolve(k + g, hb[g], disc[g]);
+    }
+  };
+  float4 A[G], B[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) A[g] = geom[g];
+  int32_t k = 0;
+  for (; k + 2 * G <= n; k += 2 * G) {
+    group(A, B, k, k + G);          // loads B while A is tested
+    group(B, A, k + G, k + 2 * G);  // loads the next A (geom is padded)
+  }
+  if (k + G <= n) {
+    float4 dummy[G];
+    group(A, dummy, k, k + G);
+    k += G;
+  }
+  for (; k < n; ++k) {
+    float hb, disc;
+    if (test(geom[k], hb, disc) < 0) resolve(k, hb, disc);
+  }
+  t_hit = t_max;
+  return best;
+}
+
+// Packed form (the production loop).  On gfx950 a VALU op that reads an
+// SGPR issues at HALF rate (4.07 vs 2.15 cycles per wave64 instruction,
+// tools/valubench2.hip), while v_pk_fma_f32 — two FMAs per lane — issues at
+// 4.1 cycles with or without an SGPR-pair operand.  So spheres are processed
+// in PAIRS: pair q holds {cx, cy, cz, S} of spheres 2q and 2q+1 as float2s
+// (SoA within the pair, 32 B), the ray terms are broadcast to both halves,
+// and each of the 8 FMA-class ops per sphere becomes half of one
+// v_pk_fma_f32.  Each half is an IEEE fma, so results are bit-identical to
+// hit_world_grouped (and to the oracle).  Scenes are padded to a multiple of
+// 2*GP spheres with a dummy {0, 0, 0, 1e30} that can never be a candidate.
+typedef float f2v __attribute__((ext_vector_type(2)));
+struct SpherePair {
+  f2v cx, cy, cz, S;
+};
+constexpr float kDummyS = 1e30f;
+
+template <int GP>
+__device__ __forceinline__ int32_t hit_world_packed(const SpherePair *__restrict__ pairs, int32_t npairs, V3<float> o,
+                                                    V3<float> d, float &t_hit
+#if RTMI_STATS
+                                                    , unsigned *stats
+#endif
+                                                    ) {
+  const float a = dot<true>(d, d);
+  const float inv_a = 1.0f / a;
+  const float K = dot<true>(o, d);
+  const float aL = a * dot<true>(o, o);
+  const float n2a = -2.0f * a;
+  const f2v DX = {d.x, d.x}, DY = {d.y, d.y}, DZ = {d.z, d.z}, KK = {K, K};
+  const f2v MX = {n2a * o.x, n2a * o.x}, MY = {n2a * o.y, n2a * o.y}, MZ = {n2a * o.z, n2a * o.z};
+  const f2v AA = {a, a}, AL = {aL, aL};
+  const float t_min = 0.001f;
+  float t_max = INFINITY;
+  int32_t best = -1;
+  auto resolve = [&](int32_t idx, float hb, float disc) {
+    const float sq = dsqrt(disc);
+    float root = (-hb - sq) * inv_a;
+    bool ok = !(root < t_min || t_max < root);
+    if (!ok) {
+      root = (-hb + sq) * inv_a;
+      ok = !(root < t_min || t_max < root);
+    }
+    if (ok) {
+      t_max = root;
+      best = idx;
+    }
+  };
+#if RTMI_PREFETCH
+  // software pipeline (see hit_world_pipelined): the next group's scalar
+  // loads are issued right after this group's first pk_fma has forced the
+  // wait for this group, so they land while this group is computed.
+  SpherePair nxt[GP];
+#pragma unroll
+  for (int g = 0; g < GP; ++g) nxt[g] = pairs[g];
+#endif
+  for (int32_t q = 0; q < npairs; q += GP) {
+    SpherePair p[GP];
+#if RTMI_PREFETCH
+#pragma unroll
+    for (int g = 0; g < GP; ++g) p[g] = nxt[g];
+    f2v h0 = __builtin_elementwise_fma(-p[0].cz, DZ, KK);
+    asm volatile("" ::"v"(h0) : "memory");  // h0 (and so the wait for p) before the next loads
+#pragma unroll
+    for (int g = 0; g < GP; ++g) nxt[g] = pairs[q + GP + g];  // padded by GP pairs
+    asm volatile("" ::: "memory");
+#else
+#pragma unroll
+    for (int g = 0; g < GP; ++g) p[g] = pairs[q + g];
+#endif
+    f2v hb[GP], disc[GP];
+    int ci[2 * GP];
+    int any = 0;
+#pragma unroll
+    for (int g = 0; g < GP; ++g) {
+#if RTMI_PREFETCH
+      const f2v hz = g == 0 ? h0 : __builtin_elementwise_fma(-p[g].cz, DZ, KK);
+#else
+      const f2v hz = __builtin_elementwise_fma(-p[g].cz, DZ, KK);
+#endif
+      hb[g] = __builtin_elementwise_fma(-p[g].cx, DX, __builtin_elementwise_fma(-p[g].cy, DY, hz));
+      const f2v acc = __builtin_elementwise_fma(MX, p[g].cx, __builtin_elementwise_fma(MY, p[g].cy,
+                      __builtin_elementwise_fma(MZ, p[g].cz, __builtin_elementwise_fma(AA, p[g].S, AL))));
+      disc[g] = __builtin_elementwise_fma(hb[g], hb[g], -acc);
+#if RTMI_DISC_ONLY
+      // candidate iff disc >= +0 (sign clear): the full test resolves the rest
+      ci[2 * g] = ~__float_as_int(disc[g].x);
+      ci[2 * g + 1] = ~__float_as_int(disc[g].y);
+#else
+      ci[2 * g] = (__float_as_int(hb[g].x) | __float_as_int(acc.x)) & ~__float_as_int(disc[g].x);
+      ci[2 * g + 1] = (__float_as_int(hb[g].y) | __float_as_int(acc.y)) & ~__float_as_int(disc[g].y);
+#endif
+      any |= ci[2 * g] | ci[2 * g + 1];
+    }
+#if RTMI_STATS
+    stats[0] += 1;
+    if (__ballot(any < 0)) stats[1] += 1;
+#endif
+    if (any < 0) {
+#pragma unroll
+      for (int g = 0; g < GP; ++g) {
+        if (ci[2 * g] < 0) resolve(2 * (q + g), hb[g].x, disc[g].x);
+        if (ci[2 * g + 1] < 0) resolve(2 * (q + g) + 1, hb[g].y, disc[g].y);
+      }
+    }
+  }
+  t_hit = t_max;
+  return best;
+}
+
+// material::scatter material.h:15-97.  Returns true if the ray scattered.
+template <bool F, class R, class G>
+__device__ __forceinline__ bool scatter(const SceneView<R> &sc, int32_t k, V3<R> din, V3<R> normal,
+                                        bool front, G &g, V3<R> &atten, V3<R> &dout) {
+  const auto s0 = sc.sh0[k];
+  const auto s1 = sc.sh1[k];
+  const int kind = int(s1.x);
+  if (kind == RT_MAT_LAMBERTIAN) {  // material.h:19-31
+    const V3<R> ru = unit<F>(in_sphere<F, R>(g));
+    V3<R> dir = mk(normal.x + ru.x, normal.y + ru.y, normal.z + ru.z);
+    if (near_zero(dir)) dir = normal;
+    dout = dir;
+    atten = mk(s0.y, s0.z, s0.w);
+    return true;
+  }
+  if (kind == RT_MAT_METAL) {  // material.h:40-49
+    const V3<R> refl = reflect<F>(unit<F>(din), normal);
+    const V3<R> rv = in_sphere<F, R>(g);
+    const R fz = s1.y;
+    const V3<R> dir = mk(madd<F>(fz, rv.x, refl.x), madd<F>(fz, rv.y, refl.y), madd<F>(fz, rv.z, refl.z));
+    dout = dir;
+    atten = mk(s0.y, s0.z, s0.w);
+    return dot<F>(dir, normal) > R(0);
+  }
+  // dielectric material.h:60-85
+  atten = mk(R(1), R(1), R(1));
+  const R ratio = front ? s1.w : s1.z;
+  const V3<R> ud = unit<F>(din);
+  const R cos_theta = dfmin(dot<F>(mk(-ud.x, -ud.y, -ud.z), normal), R(1));
+  const R sin_theta = dsqrt(madd<F>(-cos_theta, cos_theta, R(1)));
+  const bool cannot_refract = ratio * sin_theta > R(1);
+  if (cannot_refract || reflectance<F>(cos_theta, ratio) > R(g.uni()))
+    dout = reflect<F>(ud, normal);
+  else
+    dout = refract<F>(ud, normal, ratio, cos_theta);
+  return true;
+}
+
+// Hit record (sphere.h:43-53, hittable.h:23-26) for sphere k at t.
+template <bool F, class R>
+__device__ __forceinline__ void hit_record(const SceneView<R> &sc, int32_t k, V3<R> o, V3<R> d, R t,
+                                           V3<R> &p, V3<R> &normal, bool &front) {
+  const auto g = sc.geom[k];
+  const R inv_r = sc.sh0[k].x;
+  p = mk(madd<F>(t, d.x, o.x), madd<F>(t, d.y, o.y), madd<F>(t, d.z, o.z));  // ray::at ray.h:15
+  const V3<R> outward = scale(inv_r, mk(p.x - g.x, p.y - g.y, p.z - g.z));
+  front = dot<F>(d, outward) < R(0);
+  normal = front ? outward : mk(-outward.x, -outward.y, -outward.z);
+}
+
+// sky, main.cpp:80-82
+template <bool F, class R> __device__ __forceinline__ V3<R> sky(V3<R> d) {
+  const R uy = (R(1) / dsqrt(dot<F>(d, d))) * d.y;
+  const R t = R(0.5) * (uy + R(1));
+  return mk(madd<F>(t, R(0.5), R(1) - t), madd<F>(t, R(0.7), R(1) - t), madd<F>(t, R(1), R(1) - t));
+}
+
+}  // namespace rtmi

@@ -94,6 +94,7 @@ void or_fast_rng(uint64_t seed, uint64_t pixel, uint32_t sample, int32_t n, uint
 /* ref instantiation: double, no FMA, glibc stream, recursion order.        */
 /* ---------------------------------------------------------------------- */
 #define RAY_OFFSET 0
+#define HIT_EXPANDED 0
 #define PFX(x) ref_##x
 #define R double
 #define MADD(a, b, c) ((a) * (b) + (c))
@@ -118,6 +119,7 @@ void or_fast_rng(uint64_t seed, uint64_t pixel, uint32_t sample, int32_t n, uint
 #undef ROOT
 #undef T_STACK
 #undef RAY_OFFSET
+#undef HIT_EXPANDED
 
 /* ---------------------------------------------------------------------- */
 /* fast instantiation: float, fmaf policy, xoroshiro, forward product.      */
@@ -128,6 +130,7 @@ static inline float pow5f(float x) {
   return x4 * x;
 }
 #define RAY_OFFSET 1
+#define HIT_EXPANDED 1
 #define PFX(x) fast_##x
 #define R float
 #define MADD(a, b, c) fmaf((a), (b), (c))

@@ -87,6 +87,7 @@ def main():
     import torch.distributed as dist
 
     import a_dive_into_ray_tracing_amd as rt
+    from a_dive_into_ray_tracing_amd import dist as rdist
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -102,9 +103,9 @@ def main():
     world = rt.random_scene()
     cam = rt.final_camera(W / H)
     r = rt.Renderer(world, local_rank, tile_w=args.tile_w, chunk=args.chunk)
-    nrows = (H + N - 1) // N
+    row0, row_step, nrows = rdist.strip_rows(H, rank, N)  # interleaved rows, row j -> rank j % N
     strip = torch.empty((nrows, W, 3), dtype=torch.float32, device=dev)
-    gather = [torch.empty_like(strip) for _ in range(N)] if (N > 1 and rank == 0) else None
+    gathered = None
     # a non-default stream: the kernel, its HIP events and the RCCL gather
     # are all ordered on it (the null stream would bypass the events)
     stream = torch.cuda.Stream(dev)
@@ -116,12 +117,13 @@ def main():
         if record:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        r.render_rows(cam, W, H, SPP, DEPTH, SEED, rank, N, nrows, strip.data_ptr(), stream.cuda_stream)
+        nonlocal gathered
+        r.render_rows(cam, W, H, SPP, DEPTH, SEED, row0, row_step, nrows, strip.data_ptr(), stream.cuda_stream)
         if record:
             e1.record(stream)
             ev.append((e0, e1))
         if N > 1:  # the single exchange step: strips -> rank 0 over RCCL/xGMI
-            dist.gather(strip, gather_list=gather, dst=0)
+            gathered = rdist.gather_strips(strip, rank, N, dst=0)
 
     for _ in range(args.warmup):
         step(False)
@@ -154,6 +156,9 @@ def main():
     else:
         total_segs, kernel_ms_max = float(segs), kernel_ms
 
+    if rank == 0 and N > 1:  # the gathered image is whole: every row rendered, none twice
+        img = rdist.unpermute([g.cpu().numpy() for g in gathered], H)
+        assert np.isfinite(img).all() and (img.reshape(H, -1).max(axis=1) > 0).all(), "incomplete gathered image"
     if rank == 0:
         samples = W * H * SPP
         value = samples * args.steps / elapsed / 1e6

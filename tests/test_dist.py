@@ -1,0 +1,79 @@
+"""Multi-process path on the CPU: world_size 2 (and 3) over gloo.
+
+Each rank renders its interleaved row strip (here with the fast-mode oracle,
+because the product renderer needs a GPU; the partition, the one gather and
+the un-permute are the product code bench.py runs over RCCL), rank 0 gathers
+and un-permutes, and the image must equal the single-process render bit for
+bit (partition invariance).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from a_dive_into_ray_tracing_amd import dist as rdist
+
+W, H, S = 24, 17, 2  # H not a multiple of the world size: padded strips
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_path):
+    import oracle_py as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc, _ = O.final_scene()
+    cam = O.final_camera(W / H)
+    row0, step, nrows = rdist.strip_rows(H, rank, world)
+    strip = torch.from_numpy(O.fast_render(sc, cam, W, H, S, 50, 1984, row0=row0, row_step=step, nrows=nrows).copy())
+    strips = rdist.gather_strips(strip, rank, world)
+    if rank == 0:
+        np.save(out_path, rdist.unpermute([s.numpy() for s in strips], H))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_interleaved_strips_gather_to_single_process_image(world, tmp_path):
+    import oracle_py as O
+
+    out = str(tmp_path / "img.npy")
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    got = np.load(out)
+    sc, _ = O.final_scene()
+    want = O.fast_render(sc, O.final_camera(W / H), W, H, S, 50, 1984)
+    assert np.array_equal(got, want)
+
+
+def test_strip_rows_cover_every_row_once():
+    for H_, N in [(800, 8), (800, 3), (17, 4), (5, 8)]:
+        seen = []
+        for r in range(N):
+            row0, step, nrows = rdist.strip_rows(H_, r, N)
+            assert nrows == (H_ + N - 1) // N
+            seen += [row0 + k * step for k in range(nrows) if row0 + k * step < H_]
+        assert sorted(seen) == list(range(H_))
+
+
+def test_unpermute_inverts_partition():
+    img = np.random.default_rng(0).random((11, 5, 3)).astype(np.float32)
+    N = 4
+    nrows = (11 + N - 1) // N
+    strips = []
+    for g in range(N):
+        s = np.zeros((nrows, 5, 3), np.float32)
+        rows = list(range(g, 11, N))
+        s[: len(rows)] = img[rows]
+        strips.append(s)
+    assert np.array_equal(rdist.unpermute(strips, 11), img)

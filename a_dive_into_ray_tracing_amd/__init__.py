@@ -145,6 +145,14 @@ class Renderer:
     def set_tuning(self, tile_w=8, chunk=0):
         check(self.L.rt_ctx_set_tuning(self._h, tile_w, chunk), "rt_ctx_set_tuning")
 
+    def set_schedule(self, chunk=0, tail_spp=-1, tail_chunk=0):
+        check(self.L.rt_ctx_set_schedule(self._h, chunk, tail_spp, tail_chunk), "rt_ctx_set_schedule")
+
+    KERNELS = {"grid": 0, "persistent": 1}  # RT_KERNEL_* (include/rtmi.h)
+
+    def set_kernel(self, kind="persistent"):
+        check(self.L.rt_ctx_set_kernel(self._h, self.KERNELS[kind]), "rt_ctx_set_kernel")
+
     def render(self, cam, W, H, spp, max_depth=50, seed=1984):
         """Whole image, host float32 sums [H, W, 3], row 0 = bottom (main.cpp:274)."""
         out = np.zeros(W * H * 3, np.float32)

@@ -59,6 +59,8 @@ SIGNATURES = {
     "rt_ctx_destroy": (C.c_int, [C.c_void_p]),
     "rt_ctx_set_scene": (C.c_int, [C.c_void_p, C.POINTER(RtScene)]),
     "rt_ctx_set_tuning": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    "rt_ctx_set_schedule": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
+    "rt_ctx_set_kernel": (C.c_int, [C.c_void_p, C.c_int32]),
     "rt_render": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_uint64, _fp]),
     "rt_render_rows": (
         C.c_int,

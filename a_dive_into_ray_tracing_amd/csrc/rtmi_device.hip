@@ -50,12 +50,22 @@ struct RenderArgs {
   int32_t n, npairs, W, H, spp, max_depth;
   uint64_t seed;
   int32_t row0, row_step, nrows_valid;
-  int32_t tiles_x, chunk, n_chunks, n_items;
+  int32_t tiles_x, n_items;
+  // two-phase schedule: phase 1 = samples [0, spp1) in
+  // chunks of chunk1, phase 2 = [spp1, spp) in chunks of chunk2; phase-2 items
+  // come last in the grid, so the dispatch tail is one short item
+  int32_t tiles, spp1, chunk1, nch1, chunk2, nch2;
 };
 
-constexpr int kWavesPerBlock = 4;
+#ifndef RTMI_WAVES_PER_BLOCK
+#define RTMI_WAVES_PER_BLOCK 4
+#endif
+constexpr int kWavesPerBlock = RTMI_WAVES_PER_BLOCK;
 #ifndef RTMI_WAVES_PER_EU
 #define RTMI_WAVES_PER_EU 1
+#endif
+#ifndef RTMI_PERSIST_MIN_BLOCKS
+#define RTMI_PERSIST_MIN_BLOCKS 1
 #endif
 #ifndef RTMI_PAIR_GROUP
 #define RTMI_PAIR_GROUP 4
@@ -78,14 +88,21 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
   const int item = blockIdx.x * kWavesPerBlock + wave;
   if (item >= a.n_items) return;  // wave-uniform; no block barrier follows
 
-  const int tile = item / a.n_chunks;
-  const int chunk = item - tile * a.n_chunks;
+  int tile, s0, ns;
+  if (item < a.tiles * a.nch1) {
+    tile = item / a.nch1;
+    s0 = (item - tile * a.nch1) * a.chunk1;
+    ns = min(a.chunk1, a.spp1 - s0);
+  } else {
+    const int i2 = item - a.tiles * a.nch1;
+    tile = i2 / a.nch2;
+    s0 = a.spp1 + (i2 - tile * a.nch2) * a.chunk2;
+    ns = min(a.chunk2, a.spp - s0);
+  }
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
   const int x0 = tx * TW, y0 = ty * TH;
   const int vw = min(TW, a.W - x0), vh = min(TH, a.nrows_valid - y0);
   const int nv = vw * vh;  // valid pixels of this tile
-  const int s0 = chunk * a.chunk;
-  const int ns = min(a.chunk, a.spp - s0);
   const int nq = nv * ns;  // jobs: (pixel, sample) pairs of this item
 
   acc[wave][0][lane] = 0;
@@ -198,6 +215,203 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
   }
 }
 
+// ---------------------------------------------------------------------------
+// persistent render kernel: continuous per-wave job stream over work items
+// ---------------------------------------------------------------------------
+// A fixed grid of waves pulls work items (tile, sample range) from a global
+// counter.  A wave holds two items at a time in two LDS accumulator slots:
+// lanes take jobs from the current item; when it has no jobs left the wave
+// fetches the next item into the other slot and keeps its lanes busy, while
+// the paths of the previous item finish; that slot is flushed (one global
+// atomic per pixel and channel) as soon as none of its paths is in flight.
+// So no lane waits for the slowest path of an item, and the grid's tail is a
+// few paths long.  Same per-path arithmetic as render_kernel (bit-identical).
+struct ItemDesc {
+  int x0, y0, vw, nv, s0, nq;
+};
+
+template <int TW>
+__device__ __forceinline__ ItemDesc describe_item(const RenderArgs &a, int item) {
+  constexpr int TH = 64 / TW;
+  int tile, s0, ns;
+  if (item < a.tiles * a.nch1) {
+    tile = item / a.nch1;
+    s0 = (item - tile * a.nch1) * a.chunk1;
+    ns = min(a.chunk1, a.spp1 - s0);
+  } else {
+    const int i2 = item - a.tiles * a.nch1;
+    tile = i2 / a.nch2;
+    s0 = a.spp1 + (i2 - tile * a.nch2) * a.chunk2;
+    ns = min(a.chunk2, a.spp - s0);
+  }
+  const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
+  ItemDesc r;
+  r.x0 = tx * TW;
+  r.y0 = ty * TH;
+  r.vw = min(TW, a.W - r.x0);
+  const int vh = min(TH, a.nrows_valid - r.y0);
+  r.nv = r.vw * vh;
+  r.s0 = s0;
+  r.nq = r.nv * ns;
+  return r;
+}
+
+template <int TW, bool CHUNKED>
+__global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void render_persistent(
+    const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1,
+    const SpherePair *__restrict__ pairs, RenderArgs a, unsigned long long *__restrict__ accum,
+    float *__restrict__ out, unsigned long long *__restrict__ segments, unsigned *__restrict__ counter) {
+  __shared__ unsigned long long acc[kWavesPerBlock][2][3][64];
+  __shared__ unsigned long long wave_segs[kWavesPerBlock];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  for (int s = 0; s < 2; ++s)
+    for (int c = 0; c < 3; ++c) acc[wave][s][c][lane] = 0;
+  if (lane == 0) wave_segs[wave] = 0;
+  unsigned nseg = 0;
+#if RTMI_STATS
+  unsigned stats[3] = {0, 0, 0};
+#endif
+  const SceneView<float> sc{geom, sh0, sh1, a.n};
+
+  // wave-uniform slot state: the current item (slot `cur`) hands out jobs;
+  // the previous one (slot cur^1, all jobs handed out) may still have paths
+  // in flight.  Fixed-name variables, no arrays: they stay in SGPRs.
+  int cur = 0;
+  bool cur_valid = false, prev_valid = false, exhausted = false;
+  int cur_next = 0;
+  ItemDesc cd{0, 0, 1, 0, 0, 0}, pd{0, 0, 1, 0, 0, 0};
+
+  // per-lane path state
+  V3<float> o, d, T;
+  int px = 0, depth = 0, lane_slot = 0;
+  bool active = false;
+  Xoro rng;
+
+  auto flush = [&](int s, const ItemDesc &it) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (lane < it.nv) {
+      const int ly = lane / it.vw, lx = lane - ly * it.vw;
+      const size_t o3 = (size_t(it.y0 + ly) * size_t(a.W) + size_t(it.x0 + lx)) * 3;
+      for (int c = 0; c < 3; ++c) {
+        const unsigned long long v = acc[wave][s][c][lane];
+        if constexpr (CHUNKED) atomicAdd(&accum[o3 + c], v);
+        else out[o3 + c] = from_fixed((long long)v);
+      }
+    }
+    for (int c = 0; c < 3; ++c) acc[wave][s][c][lane] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  };
+
+  for (;;) {
+    // 1. hand jobs to idle lanes, fetching items as the current one runs dry
+    unsigned long long idle = __ballot(!active);
+    while (idle) {
+      if (cur_valid && cur_next < cd.nq) {
+        const int avail = cd.nq - cur_next;
+        const int rank = __builtin_amdgcn_mbcnt_hi(unsigned(idle >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(idle), 0u));
+        if (((idle >> lane) & 1ull) && rank < avail) {
+          // job q -> pixel q % nv, sample s0 + q / nv; then the camera ray
+          const int q = cur_next + rank;
+          const int qs = q / cd.nv;
+          px = q - qs * cd.nv;
+          const int ly = px / cd.vw, lx = px - ly * cd.vw;
+          const int i = cd.x0 + lx;
+          const int j = a.row0 + (cd.y0 + ly) * a.row_step;
+          rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(cd.s0 + qs));
+          const float u = (float(i) + rng.uni()) / float(a.W - 1);  // main.cpp:278
+          const float v = (float(j) + rng.uni()) / float(a.H - 1);  // main.cpp:279
+          get_ray<true, float>(a.cam, u, v, rng, o, d);
+          T = mk(1.f, 1.f, 1.f);
+          depth = 0;
+          lane_slot = cur;
+          active = true;
+        }
+        cur_next += min(__popcll(idle), avail);
+        idle = __ballot(!active);
+      } else {
+        if (prev_valid || exhausted) break;  // wait for the previous item to drain
+        unsigned itn = 0;
+        if (lane == 0) itn = atomicAdd(counter, 1u);
+        itn = __shfl(itn, 0);
+        if (int(itn) >= a.n_items) {
+          exhausted = true;
+          break;
+        }
+        prev_valid = cur_valid;  // all its jobs are handed out
+        pd = cd;
+        cur ^= 1;
+        cd = describe_item<TW>(a, int(itn));
+        cur_valid = true;
+        cur_next = 0;
+      }
+    }
+    if (__ballot(active) == 0) break;
+
+    // 2. one segment of every live path
+    bool done = false;
+    V3<float> col = mk(0.f, 0.f, 0.f);
+    if (active) {
+      float t;
+      ++nseg;
+      const int k = hit_world_packed<kPairGroup>(pairs, a.npairs, o, d, t
+#if RTMI_STATS
+                                                 , stats
+#endif
+      );
+      if (k < 0) {
+        const V3<float> sk = sky<true, float>(d);
+        col = mk(T.x * sk.x, T.y * sk.y, T.z * sk.z);
+        done = true;
+      } else {
+        V3<float> p, nrm, at, nd;
+        bool front;
+        hit_record<true, float>(sc, k, o, d, t, p, nrm, front);
+        if (!scatter<true, float>(sc, k, d, nrm, front, rng, at, nd)) {
+          done = true;
+        } else {
+          T = mk(T.x * at.x, T.y * at.y, T.z * at.z);
+          float m = __builtin_fabsf(p.x);  // ray offset, DESIGN.md §3.3
+          if (__builtin_fabsf(p.y) > m) m = __builtin_fabsf(p.y);
+          if (__builtin_fabsf(p.z) > m) m = __builtin_fabsf(p.z);
+          float delta = 0x1p-14f * (1.0f + m);
+          if (dot<true>(nd, nrm) < 0.f) delta = -delta;
+          o = mk(__builtin_fmaf(delta, nrm.x, p.x), __builtin_fmaf(delta, nrm.y, p.y), __builtin_fmaf(delta, nrm.z, p.z));
+          d = nd;
+          if (++depth >= a.max_depth) done = true;
+        }
+      }
+    }
+    // 3. finished paths add their colour to their item's slot
+    if (done) {
+      atomicAdd(&acc[wave][lane_slot][0][px], (unsigned long long)to_fixed(col.x));
+      atomicAdd(&acc[wave][lane_slot][1][px], (unsigned long long)to_fixed(col.y));
+      atomicAdd(&acc[wave][lane_slot][2][px], (unsigned long long)to_fixed(col.z));
+      active = false;
+    }
+    // 4. flush items whose jobs are all handed out and whose paths are all done
+    if (prev_valid && __ballot(active && lane_slot != cur) == 0) {
+      flush(cur ^ 1, pd);
+      prev_valid = false;
+    }
+    if (cur_valid && cur_next >= cd.nq && __ballot(active && lane_slot == cur) == 0) {
+      flush(cur, cd);
+      cur_valid = false;
+    }
+  }
+  if (prev_valid) flush(cur ^ 1, pd);
+  if (cur_valid) flush(cur, cd);
+
+  atomicAdd(&wave_segs[wave], (unsigned long long)nseg);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) atomicAdd(segments, wave_segs[wave]);
+#if RTMI_STATS
+  if (lane == 0) { atomicAdd(&segments[1], (unsigned long long)stats[0]); atomicAdd(&segments[2], (unsigned long long)stats[1]); }
+  atomicAdd(&segments[3], (unsigned long long)stats[2]);
+#endif
+}
+
 __global__ void finalize_kernel(const unsigned long long *__restrict__ accum, float *__restrict__ out, size_t n) {
   const size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i < n) out[i] = from_fixed((long long)accum[i]);
@@ -294,9 +508,14 @@ struct rt_ctx {
   float *scratch = nullptr;
   size_t scratch_cap = 0;  // elements
   unsigned long long *segments = nullptr;  // world.hit calls of the last render
+  unsigned *counter = nullptr;             // persistent kernel's work-item counter
+  int32_t persistent = 1;                  // 1: render_persistent, 0: one wave per item
+  int32_t resident_blocks = 0;             // blocks of the persistent grid (from the occupancy query)
   hipStream_t last_stream = nullptr;
   int32_t tile_w = 8;
-  int32_t chunk = 0;
+  int32_t chunk = 0;       // phase-1 samples per item (0 = automatic)
+  int32_t tail_spp = -1;   // samples in the short-item phase (-1 = automatic)
+  int32_t tail_chunk = 0;  // phase-2 samples per item (0 = automatic)
 };
 
 namespace rtmi {
@@ -376,6 +595,15 @@ RTMI_EXPORT int rt_ctx_create(int32_t device, rt_ctx **out) {
   HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
   if (int rc = dev_alloc(&ctx->segments, 4)) return rc;
   HIP_TRY(hipMemset(ctx->segments, 0, 4 * sizeof(unsigned long long)));
+  if (int rc = dev_alloc(&ctx->counter, 1)) return rc;
+  {
+    // resident blocks per CU for the persistent grid; over-subscription is
+    // harmless (extra waves start later and find the counter exhausted)
+    int per_cu = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<8, true>,
+                                                         64 * kWavesPerBlock, 0));
+    ctx->resident_blocks = std::max(1, per_cu) * prop.multiProcessorCount;
+  }
   *out = ctx.release();
   return RT_OK;
 }
@@ -385,7 +613,7 @@ RTMI_EXPORT int rt_ctx_destroy(rt_ctx *ctx) {
   DeviceGuard guard(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   for (void *p : {(void *)ctx->geom, (void *)ctx->sh0, (void *)ctx->sh1, (void *)ctx->geom64, (void *)ctx->sh064,
-                  (void *)ctx->sh164, (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments, (void *)ctx->pairs})
+                  (void *)ctx->sh164, (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments, (void *)ctx->pairs, (void *)ctx->counter})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -449,6 +677,22 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
   return RT_OK;
 }
 
+RTMI_EXPORT int rt_ctx_set_schedule(rt_ctx *ctx, int32_t chunk, int32_t tail_spp, int32_t tail_chunk) {
+  if (!ctx) return set_error(RT_EINVAL, "null ctx");
+  if (chunk < 0 || tail_chunk < 0) return set_error(RT_EINVAL, "chunk sizes must be >= 0");
+  ctx->chunk = chunk;
+  ctx->tail_spp = tail_spp;
+  ctx->tail_chunk = tail_chunk;
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind) {
+  if (!ctx) return set_error(RT_EINVAL, "null ctx");
+  if (kind != RT_KERNEL_GRID && kind != RT_KERNEL_PERSISTENT) return set_error(RT_EINVAL, "unknown kernel kind");
+  ctx->persistent = kind == RT_KERNEL_PERSISTENT;
+  return RT_OK;
+}
+
 RTMI_EXPORT int rt_ctx_set_tuning(rt_ctx *ctx, int32_t tile_w, int32_t chunk) {
   if (!ctx) return set_error(RT_EINVAL, "null ctx");
   if (tile_w != 8 && tile_w != 16 && tile_w != 32 && tile_w != 64)
@@ -460,6 +704,17 @@ RTMI_EXPORT int rt_ctx_set_tuning(rt_ctx *ctx, int32_t tile_w, int32_t chunk) {
 }
 
 namespace {
+
+template <int TW>
+void launch_persistent(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a,
+                       unsigned long long *accum, float *out) {
+  if (chunked)
+    hipLaunchKernelGGL((render_persistent<TW, true>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
+                       ctx->sh1, ctx->pairs, a, accum, out, ctx->segments, ctx->counter);
+  else
+    hipLaunchKernelGGL((render_persistent<TW, false>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
+                       ctx->sh1, ctx->pairs, a, accum, out, ctx->segments, ctx->counter);
+}
 
 template <int TW>
 void launch_tw(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a,
@@ -493,19 +748,27 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   const int tiles_x = (W + TW - 1) / TW;
   const int tiles_y = (nvalid + TH - 1) / TH;
   const int64_t tiles = int64_t(tiles_x) * tiles_y;
-  // Work items: enough waves to fill 256 CUs several times over, and short
-  // enough that the dispatch tail stays small.
-  int32_t chunk = ctx->chunk;
-  if (chunk <= 0) {
-    const int64_t want_items = 256 * 8 * 16;
-    int64_t n_chunks = std::max<int64_t>(1, (want_items + tiles - 1) / tiles);
-    n_chunks = std::min<int64_t>(n_chunks, spp);
-    chunk = int32_t((spp + n_chunks - 1) / n_chunks);
-    chunk = std::max(chunk, std::min<int32_t>(spp, 32));  // keep items long enough to amortise the flush
+  // Work items: phase 1 covers the first spp1 samples in
+  // long items (chunk1: few per-item ramp-down tails and accumulator flushes),
+  // phase 2 the rest in short items (chunk2) that run last, so the grid's
+  // dispatch tail is one short item.
+  // Automatic: ~150 k items (about 24 per resident wave slot on 256 CUs),
+  // items of 16..64 samples; measured on config 2: chunk 50 -> 128.4 ms,
+  // 100 -> 133, 167 -> 143, 500 -> 193, 25 -> 133, 10 -> 149.
+  int32_t chunk1 = ctx->chunk, chunk2 = ctx->tail_chunk, tail = ctx->tail_spp;
+  if (chunk1 <= 0) {
+    const int64_t want_items = 150000;
+    chunk1 = int32_t(std::min<int64_t>(64, std::max<int64_t>(16, tiles * int64_t(spp) / want_items)));
   }
-  chunk = std::min(chunk, spp);
-  const int32_t n_chunks = (spp + chunk - 1) / chunk;
-  const int64_t items = tiles * n_chunks;
+  if (chunk2 <= 0) chunk2 = std::max(1, chunk1 / 4);
+  if (tail < 0) tail = 0;  // automatic: no short-item phase (it measured no better)
+  chunk1 = std::min(chunk1, spp);
+  tail = std::min(tail, spp);
+  const int32_t spp1 = spp - tail;
+  const int32_t nch1 = spp1 > 0 ? (spp1 + chunk1 - 1) / chunk1 : 0;
+  chunk2 = std::min(chunk2, std::max(tail, 1));
+  const int32_t nch2 = tail > 0 ? (tail + chunk2 - 1) / chunk2 : 0;
+  const int64_t items = tiles * (int64_t(nch1) + nch2);
   if (items > int64_t(INT32_MAX) - kWavesPerBlock) return set_error(RT_EINVAL, "too many work items");
   RenderArgs a;
   a.cam = cam_f(cam);
@@ -513,8 +776,9 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   a.npairs = ctx->npairs;
   a.W = W; a.H = H; a.spp = spp; a.max_depth = max_depth; a.seed = seed;
   a.row0 = row0; a.row_step = row_step; a.nrows_valid = nvalid;
-  a.tiles_x = tiles_x; a.chunk = chunk; a.n_chunks = n_chunks; a.n_items = int32_t(items);
-  const bool chunked = n_chunks > 1;
+  a.tiles_x = tiles_x; a.n_items = int32_t(items);
+  a.tiles = int32_t(tiles); a.spp1 = spp1; a.chunk1 = chunk1; a.nch1 = nch1; a.chunk2 = chunk2; a.nch2 = nch2;
+  const bool chunked = nch1 + nch2 > 1;
   const size_t n_valid_out = size_t(nvalid) * W * 3;
   if (chunked) {
     if (ctx->accum_cap < n_valid_out) {
@@ -524,12 +788,25 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     }
     HIP_TRY(hipMemsetAsync(ctx->accum, 0, n_valid_out * sizeof(unsigned long long), st));
   }
-  const dim3 grid(unsigned((items + kWavesPerBlock - 1) / kWavesPerBlock));
-  switch (TW) {
-    case 8: launch_tw<8>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
-    case 16: launch_tw<16>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
-    case 32: launch_tw<32>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
-    default: launch_tw<64>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
+  if (ctx->persistent) {
+    // a resident grid of waves pulling items from a global counter
+    HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
+    const int64_t waves = std::min<int64_t>(items, int64_t(ctx->resident_blocks) * kWavesPerBlock);
+    const dim3 grid(unsigned((waves + kWavesPerBlock - 1) / kWavesPerBlock));
+    switch (TW) {
+      case 8: launch_persistent<8>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
+      case 16: launch_persistent<16>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
+      case 32: launch_persistent<32>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
+      default: launch_persistent<64>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
+    }
+  } else {
+    const dim3 grid(unsigned((items + kWavesPerBlock - 1) / kWavesPerBlock));
+    switch (TW) {
+      case 8: launch_tw<8>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
+      case 16: launch_tw<16>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
+      case 32: launch_tw<32>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
+      default: launch_tw<64>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
+    }
   }
   HIP_TRY(hipGetLastError());
   if (chunked) {

@@ -80,7 +80,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--tile-w", type=int, default=8)
     ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--tail-spp", type=int, default=-1)
+    ap.add_argument("--tail-chunk", type=int, default=0)
+    ap.add_argument("--kernel", choices=["persistent", "grid"], default="persistent")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--strip-of", type=int, default=0,
+                    help="analysis only: time ONE rank's interleaved strip of an N-GPU run on this GPU")
     args = ap.parse_args()
 
     import torch
@@ -103,7 +108,11 @@ def main():
     world = rt.random_scene()
     cam = rt.final_camera(W / H)
     r = rt.Renderer(world, local_rank, tile_w=args.tile_w, chunk=args.chunk)
+    r.set_schedule(args.chunk, args.tail_spp, args.tail_chunk)
+    r.set_kernel(args.kernel)
     row0, row_step, nrows = rdist.strip_rows(H, rank, N)  # interleaved rows, row j -> rank j % N
+    if args.strip_of > 1 and N == 1:  # analysis mode: one rank's share of an N-GPU render
+        row0, row_step, nrows = rdist.strip_rows(H, 0, args.strip_of)
     strip = torch.empty((nrows, W, 3), dtype=torch.float32, device=dev)
     gathered = None
     # a non-default stream: the kernel, its HIP events and the RCCL gather
@@ -160,7 +169,7 @@ def main():
         img = rdist.unpermute([g.cpu().numpy() for g in gathered], H)
         assert np.isfinite(img).all() and (img.reshape(H, -1).max(axis=1) > 0).all(), "incomplete gathered image"
     if rank == 0:
-        samples = W * H * SPP
+        samples = W * H * SPP if not args.strip_of else nrows * W * SPP
         value = samples * args.steps / elapsed / 1e6
         flop_rank = segs * FLOP_PER_SPHERE_TEST * len(world)  # this rank's launch
         achieved = flop_rank / (kernel_ms * 1e-3) / 1e12
@@ -189,6 +198,7 @@ def main():
                 "width": W, "height": H, "spp": SPP, "max_depth": DEPTH, "seed": SEED, "spheres": len(world),
                 "partition": "interleaved rows, one RCCL gather" if N > 1 else "single GPU",
                 "tile": f"{args.tile_w}x{64 // args.tile_w}",
+                "kernel": args.kernel,
             },
             "roofline": {
                 "bound": "valu",

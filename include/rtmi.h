@@ -113,6 +113,17 @@ int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene);
  * wavefront); chunk = samples per work item (0 = automatic).  Neither
  * changes the image. */
 int rt_ctx_set_tuning(rt_ctx *ctx, int32_t tile_w, int32_t chunk);
+/* Work schedule: the first spp - tail_spp samples of every tile in items of
+ * `chunk` samples, the last tail_spp in items of `tail_chunk`, dispatched
+ * last (0 / -1 = automatic).  Does not change the image. */
+int rt_ctx_set_schedule(rt_ctx *ctx, int32_t chunk, int32_t tail_spp, int32_t tail_chunk);
+
+/* Kernel shape.  RT_KERNEL_PERSISTENT (default): a resident grid of waves
+ * pulls work items from a global counter and streams paths continuously
+ * (two items in flight per wave).  RT_KERNEL_GRID: one wave per work item.
+ * Both give bit-identical images. */
+enum { RT_KERNEL_GRID = 0, RT_KERNEL_PERSISTENT = 1 };
+int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind);
 
 /* The whole image: replaces the 16-thread worker() block main.cpp:313-338.
  * Synchronous; `sum` is a HOST buffer of W*H*3 floats. */

@@ -97,14 +97,19 @@ def test_exact_replay_reproduces_reference_image(name, W, H, S, final_renderer, 
 
 
 # ------------------------------------------------------------ tier 2 -------
+@pytest.mark.parametrize("kernel", ["persistent", "grid"])
 @pytest.mark.parametrize("tile_w", [8, 16, 32, 64])
 @pytest.mark.parametrize("chunk", [0, 3, 1000])
-def test_fast_kernel_bit_exact_vs_oracle_final(tile_w, chunk, final_world, final_renderer):
+def test_fast_kernel_bit_exact_vs_oracle_final(kernel, tile_w, chunk, final_world, final_renderer):
     W, H, S = 48, 32, 8
     cam = rt.final_camera(W / H)
     final_renderer.set_tuning(tile_w, chunk)
-    got = final_renderer.render(cam, W, H, S, 50, SEED)
-    final_renderer.set_tuning(8, 0)
+    final_renderer.set_kernel(kernel)
+    try:
+        got = final_renderer.render(cam, W, H, S, 50, SEED)
+    finally:
+        final_renderer.set_tuning(8, 0)
+        final_renderer.set_kernel("persistent")
     want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
     assert np.array_equal(got, want), np.abs(got - want).max()
 
@@ -181,11 +186,34 @@ def config2(final_renderer):
 
 
 def test_config2_deterministic_and_tiling_invariant(config2, final_renderer):
+    """Same image from the other kernel shape, another tile and a two-phase
+    schedule (long items, then a 60-spp tail of 7-sample items)."""
     cam, img = config2
     final_renderer.set_tuning(64, 100)
-    again = final_renderer.render(cam, 1200, 800, 500, 50, SEED)
-    final_renderer.set_tuning(8, 0)
+    final_renderer.set_schedule(100, 60, 7)
+    final_renderer.set_kernel("grid")
+    try:
+        again = final_renderer.render(cam, 1200, 800, 500, 50, SEED)
+    finally:
+        final_renderer.set_tuning(8, 0)
+        final_renderer.set_schedule(0, -1, 0)
+        final_renderer.set_kernel("persistent")
     assert np.array_equal(img, again)
+
+
+@pytest.mark.parametrize("sched", [(2, 0, 0), (3, 37, 1)])
+def test_persistent_schedules_bit_exact_vs_oracle(sched, final_world, final_renderer):
+    """The persistent kernel with many more items than resident waves and a
+    short-item tail phase (items of two sizes in flight in one wave)."""
+    W, H, S = 160, 96, 64
+    cam = rt.final_camera(W / H)
+    final_renderer.set_schedule(*sched)  # 7680 / 12240 items: several per resident wave
+    try:
+        got = final_renderer.render(cam, W, H, S, 50, SEED)
+    finally:
+        final_renderer.set_schedule(0, -1, 0)
+    want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
+    assert np.array_equal(got, want), np.abs(got - want).max()
 
 
 def test_config2_sampled_pixels_bit_exact_vs_oracle(config2, final_world):

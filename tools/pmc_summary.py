@@ -9,7 +9,7 @@ vals = collections.defaultdict(list)
 for f in sorted(glob.glob(f"{root}/pmc*/*_counter_collection.csv")):
     per = collections.defaultdict(float)
     for r in csv.DictReader(open(f)):
-        if "render_kernel" in r["Kernel_Name"]:
+        if "render_kernel" in r["Kernel_Name"] or "render_persistent" in r["Kernel_Name"]:
             per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
     for (d, c), v in per.items():
         vals[c].append(v)

@@ -64,6 +64,39 @@ constexpr int kWavesPerBlock = RTMI_WAVES_PER_BLOCK;
 #ifndef RTMI_WAVES_PER_EU
 #define RTMI_WAVES_PER_EU 1
 #endif
+// RTMI_TRACE builds record one line per wave (analysis only): start/end
+// (s_memrealtime, 100 MHz), CU id and items taken, world.hit calls.
+#ifndef RTMI_TRACE
+#define RTMI_TRACE 0
+#endif
+#if RTMI_TRACE
+constexpr unsigned kTraceCap = 1u << 18;
+__device__ unsigned long long g_trace[kTraceCap * 4];
+__device__ unsigned g_trace_n;
+#define RTMI_TRACE_BEGIN const unsigned long long trace_t0 = __builtin_amdgcn_s_memrealtime();
+#define RTMI_TRACE_END(items)                                                            \
+  if (lane == 0) {                                                                       \
+    const unsigned k_ = atomicAdd(&g_trace_n, 1u);                                       \
+    if (k_ < kTraceCap) {                                                                \
+      g_trace[4 * k_] = trace_t0;                                                        \
+      g_trace[4 * k_ + 1] = __builtin_amdgcn_s_memrealtime();                            \
+      g_trace[4 * k_ + 2] = (uint64_t(__builtin_amdgcn_s_getreg(0xF804)) << 32) |        \
+                            uint64_t(unsigned(items));                                   \
+      g_trace[4 * k_ + 3] = (uint64_t(blockIdx.x * kWavesPerBlock + wave) << 32) |        \
+                            (wave_segs[wave] & 0xFFFFFFFFull);                           \
+    }                                                                                    \
+  }
+#else
+#define RTMI_TRACE_BEGIN
+#define RTMI_TRACE_END(items)
+#endif
+
+#ifndef RTMI_FAIR
+#define RTMI_FAIR 3
+#endif
+#ifndef RTMI_FAIR_TIME
+#define RTMI_FAIR_TIME 0
+#endif
 #ifndef RTMI_PERSIST_MIN_BLOCKS
 #define RTMI_PERSIST_MIN_BLOCKS 1
 #endif
@@ -110,13 +143,12 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
   acc[wave][2][lane] = 0;
   if (lane == 0) wave_segs[wave] = 0;
   unsigned nseg = 0;  // world.hit calls of this lane (algorithmic-work accounting)
+  RTMI_TRACE_BEGIN
 #if RTMI_STATS
   unsigned stats[3] = {0, 0, 0};  // groups, groups with a candidate (wave), resolves (lane)
 #endif
 
   const SceneView<float> sc{geom, sh0, sh1, a.n};
-  const float inv_wm1 = 0.f;  // (unused; divisions below follow main.cpp:278-279)
-  (void)inv_wm1;
 
   V3<float> o, d, T;
   int px = 0, depth = 0;
@@ -204,6 +236,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
   if (lane == 0) { atomicAdd(&segments[1], (unsigned long long)stats[0]); atomicAdd(&segments[2], (unsigned long long)stats[1]); }
   atomicAdd(&segments[3], (unsigned long long)stats[2]);
 #endif
+  RTMI_TRACE_END(1)
   if (lane < nv) {
     const int ly = lane / vw, lx = lane - ly * vw;
     const size_t o3 = (size_t(y0 + ly) * size_t(a.W) + size_t(x0 + lx)) * 3;
@@ -269,11 +302,24 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
     for (int c = 0; c < 3; ++c) acc[wave][s][c][lane] = 0;
   if (lane == 0) wave_segs[wave] = 0;
   unsigned nseg = 0;
+  int n_taken = 0;
+  RTMI_TRACE_BEGIN
 #if RTMI_STATS
   unsigned stats[3] = {0, 0, 0};
 #endif
   const SceneView<float> sc{geom, sh0, sh1, a.n};
 
+#if RTMI_FAIR == 2
+  {  // experiment: priority by hardware wave slot (inverts the age order)
+    const unsigned slot = __builtin_amdgcn_s_getreg(0xF804) & 15u;
+    if (slot >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (slot == 2) __builtin_amdgcn_s_setprio(2);
+    else if (slot == 1) __builtin_amdgcn_s_setprio(1);
+  }
+#endif
+#if RTMI_FAIR == 3
+  unsigned prio_phase = __builtin_amdgcn_s_getreg(0xF804) & 15u;  // hardware wave slot
+#endif
   // wave-uniform slot state: the current item (slot `cur`) hands out jobs;
   // the previous one (slot cur^1, all jobs handed out) may still have paths
   // in flight.  Fixed-name variables, no arrays: they stay in SGPRs.
@@ -338,6 +384,15 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
           exhausted = true;
           break;
         }
+#if RTMI_FAIR == 1
+        // The SIMD issues the oldest ready wave first, so in a resident grid
+        // some waves starve (10x spread of work per wave) and end up holding
+        // the last items alone.  A wave behind the average item count raises
+        // its issue priority until it has caught up.
+        if (n_taken * int(gridDim.x) * kWavesPerBlock < int(itn)) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(0);
+#endif
+        ++n_taken;
         prev_valid = cur_valid;  // all its jobs are handed out
         pd = cd;
         cur ^= 1;
@@ -347,6 +402,22 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
       }
     }
     if (__ballot(active) == 0) break;
+#if RTMI_FAIR == 3
+    // The SIMD issues the oldest ready wave first: in a resident grid the
+    // youngest wave of a SIMD gets ~1/10 of the oldest one's issue slots and
+    // is left holding items alone at the end.  Rotating the issue priority
+    // every segment step gives every wave the same share.
+#if RTMI_FAIR_TIME
+    switch ((unsigned(__builtin_amdgcn_s_memrealtime() >> RTMI_FAIR_TIME) + prio_phase) & 3) {
+#else
+    switch ((prio_phase++) & 3) {
+#endif
+      case 0: __builtin_amdgcn_s_setprio(0); break;
+      case 1: __builtin_amdgcn_s_setprio(1); break;
+      case 2: __builtin_amdgcn_s_setprio(2); break;
+      default: __builtin_amdgcn_s_setprio(3); break;
+    }
+#endif
 
     // 2. one segment of every live path
     bool done = false;
@@ -410,6 +481,8 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
   if (lane == 0) { atomicAdd(&segments[1], (unsigned long long)stats[0]); atomicAdd(&segments[2], (unsigned long long)stats[1]); }
   atomicAdd(&segments[3], (unsigned long long)stats[2]);
 #endif
+  RTMI_TRACE_END(n_taken)
+  (void)n_taken;
 }
 
 __global__ void finalize_kernel(const unsigned long long *__restrict__ accum, float *__restrict__ out, size_t n) {
@@ -509,7 +582,7 @@ struct rt_ctx {
   size_t scratch_cap = 0;  // elements
   unsigned long long *segments = nullptr;  // world.hit calls of the last render
   unsigned *counter = nullptr;             // persistent kernel's work-item counter
-  int32_t persistent = 1;                  // 1: render_persistent, 0: one wave per item
+  int32_t kernel = RT_KERNEL_AUTO;         // RT_KERNEL_* (rtmi.h)
   int32_t resident_blocks = 0;             // blocks of the persistent grid (from the occupancy query)
   hipStream_t last_stream = nullptr;
   int32_t tile_w = 8;
@@ -688,8 +761,9 @@ RTMI_EXPORT int rt_ctx_set_schedule(rt_ctx *ctx, int32_t chunk, int32_t tail_spp
 
 RTMI_EXPORT int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind) {
   if (!ctx) return set_error(RT_EINVAL, "null ctx");
-  if (kind != RT_KERNEL_GRID && kind != RT_KERNEL_PERSISTENT) return set_error(RT_EINVAL, "unknown kernel kind");
-  ctx->persistent = kind == RT_KERNEL_PERSISTENT;
+  if (kind != RT_KERNEL_GRID && kind != RT_KERNEL_PERSISTENT && kind != RT_KERNEL_AUTO)
+    return set_error(RT_EINVAL, "unknown kernel kind");
+  ctx->kernel = kind;
   return RT_OK;
 }
 
@@ -755,10 +829,21 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   // Automatic: ~150 k items (about 24 per resident wave slot on 256 CUs),
   // items of 16..64 samples; measured on config 2: chunk 50 -> 128.4 ms,
   // 100 -> 133, 167 -> 143, 500 -> 193, 25 -> 133, 10 -> 149.
+  // Kernel shape (automatic): the resident persistent grid wins on strips
+  // (measured, config 2 rows of 1 rank: 1/2 of the image 65.5 vs 67.3 ms,
+  // 1/4 33.4 vs 36.5, 1/8 17.9 vs 19.3); one wave per item on a whole frame
+  // (128.2 vs 130.4 ms).  Both give the same image.
+  const int64_t tile_samples = tiles * int64_t(spp);
+  const bool persistent = ctx->kernel == RT_KERNEL_PERSISTENT ||
+                          (ctx->kernel == RT_KERNEL_AUTO && tile_samples < 6000000);
   int32_t chunk1 = ctx->chunk, chunk2 = ctx->tail_chunk, tail = ctx->tail_spp;
-  if (chunk1 <= 0) {
+  if (chunk1 <= 0 && persistent) {
+    // ~28 items per resident wave (1/8 strip: chunk 8 -> 17.5 ms, 16 -> 17.9, 32 -> 19.7)
+    const int64_t waves = int64_t(ctx->resident_blocks) * kWavesPerBlock;
+    chunk1 = int32_t(std::min<int64_t>(64, std::max<int64_t>(4, tile_samples / (28 * waves))));
+  } else if (chunk1 <= 0) {
     const int64_t want_items = 150000;
-    chunk1 = int32_t(std::min<int64_t>(64, std::max<int64_t>(16, tiles * int64_t(spp) / want_items)));
+    chunk1 = int32_t(std::min<int64_t>(64, std::max<int64_t>(16, tile_samples / want_items)));
   }
   if (chunk2 <= 0) chunk2 = std::max(1, chunk1 / 4);
   if (tail < 0) tail = 0;  // automatic: no short-item phase (it measured no better)
@@ -788,7 +873,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     }
     HIP_TRY(hipMemsetAsync(ctx->accum, 0, n_valid_out * sizeof(unsigned long long), st));
   }
-  if (ctx->persistent) {
+  if (persistent) {
     // a resident grid of waves pulling items from a global counter
     HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
     const int64_t waves = std::min<int64_t>(items, int64_t(ctx->resident_blocks) * kWavesPerBlock);
@@ -924,6 +1009,26 @@ RTMI_EXPORT int rt_ctx_last_segments(rt_ctx *ctx, uint64_t *segments) {
 // Debug counters of the last render (RTMI_STATS builds only; zeros otherwise):
 // out[0] = world.hit calls, out[1] = sphere groups tested (per wave),
 // out[2] = groups where some lane had a candidate, out[3] = candidate resolves.
+// Per-wave trace of the renders since the last call (RTMI_TRACE builds; 0
+// lines otherwise): 4 u64 per wave, see RTMI_TRACE_END.  Returns the count.
+RTMI_EXPORT int rt_ctx_debug_trace(rt_ctx *ctx, uint64_t *out, int32_t cap) {
+  if (!ctx || !out) return set_error(RT_EINVAL, "null argument");
+#if RTMI_TRACE
+  DeviceGuard guard(ctx->device);
+  HIP_TRY(hipDeviceSynchronize());
+  unsigned n = 0;
+  HIP_TRY(hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_trace_n), sizeof n));
+  n = std::min<unsigned>(std::min<unsigned>(n, kTraceCap), unsigned(std::max(cap, 0)));
+  if (n) HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace), size_t(n) * 4 * sizeof(uint64_t)));
+  const unsigned zero = 0;
+  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_trace_n), &zero, sizeof zero));
+  return int(n);
+#else
+  (void)cap;
+  return 0;
+#endif
+}
+
 RTMI_EXPORT int rt_ctx_debug_counters(rt_ctx *ctx, uint64_t *out) {
   if (!ctx || !out) return set_error(RT_EINVAL, "null argument");
   DeviceGuard guard(ctx->device);

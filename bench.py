@@ -82,7 +82,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--tail-spp", type=int, default=-1)
     ap.add_argument("--tail-chunk", type=int, default=0)
-    ap.add_argument("--kernel", choices=["persistent", "grid"], default="persistent")
+    ap.add_argument("--kernel", choices=["auto", "persistent", "grid"], default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--strip-of", type=int, default=0,
                     help="analysis only: time ONE rank's interleaved strip of an N-GPU run on this GPU")

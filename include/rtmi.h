@@ -118,11 +118,12 @@ int rt_ctx_set_tuning(rt_ctx *ctx, int32_t tile_w, int32_t chunk);
  * last (0 / -1 = automatic).  Does not change the image. */
 int rt_ctx_set_schedule(rt_ctx *ctx, int32_t chunk, int32_t tail_spp, int32_t tail_chunk);
 
-/* Kernel shape.  RT_KERNEL_PERSISTENT (default): a resident grid of waves
- * pulls work items from a global counter and streams paths continuously
- * (two items in flight per wave).  RT_KERNEL_GRID: one wave per work item.
- * Both give bit-identical images. */
-enum { RT_KERNEL_GRID = 0, RT_KERNEL_PERSISTENT = 1 };
+/* Kernel shape.  RT_KERNEL_PERSISTENT: a resident grid of waves pulls work
+ * items from a global counter and streams paths continuously (two items in
+ * flight per wave).  RT_KERNEL_GRID: one wave per work item.
+ * RT_KERNEL_AUTO (default): persistent for strips, grid for whole frames.
+ * All give bit-identical images. */
+enum { RT_KERNEL_GRID = 0, RT_KERNEL_PERSISTENT = 1, RT_KERNEL_AUTO = 2 };
 int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind);
 
 /* The whole image: replaces the 16-thread worker() block main.cpp:313-338.

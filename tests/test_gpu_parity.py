@@ -109,7 +109,7 @@ def test_fast_kernel_bit_exact_vs_oracle_final(kernel, tile_w, chunk, final_worl
         got = final_renderer.render(cam, W, H, S, 50, SEED)
     finally:
         final_renderer.set_tuning(8, 0)
-        final_renderer.set_kernel("persistent")
+        final_renderer.set_kernel("auto")
     want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
     assert np.array_equal(got, want), np.abs(got - want).max()
 
@@ -191,13 +191,13 @@ def test_config2_deterministic_and_tiling_invariant(config2, final_renderer):
     cam, img = config2
     final_renderer.set_tuning(64, 100)
     final_renderer.set_schedule(100, 60, 7)
-    final_renderer.set_kernel("grid")
+    final_renderer.set_kernel("persistent")
     try:
         again = final_renderer.render(cam, 1200, 800, 500, 50, SEED)
     finally:
         final_renderer.set_tuning(8, 0)
         final_renderer.set_schedule(0, -1, 0)
-        final_renderer.set_kernel("persistent")
+        final_renderer.set_kernel("auto")
     assert np.array_equal(img, again)
 
 
@@ -208,10 +208,12 @@ def test_persistent_schedules_bit_exact_vs_oracle(sched, final_world, final_rend
     W, H, S = 160, 96, 64
     cam = rt.final_camera(W / H)
     final_renderer.set_schedule(*sched)  # 7680 / 12240 items: several per resident wave
+    final_renderer.set_kernel("persistent")
     try:
         got = final_renderer.render(cam, W, H, S, 50, SEED)
     finally:
         final_renderer.set_schedule(0, -1, 0)
+        final_renderer.set_kernel("auto")
     want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
     assert np.array_equal(got, want), np.abs(got - want).max()
 

@@ -145,7 +145,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
   unsigned nseg = 0;  // world.hit calls of this lane (algorithmic-work accounting)
   RTMI_TRACE_BEGIN
 #if RTMI_STATS
-  unsigned stats[3] = {0, 0, 0};  // groups, groups with a candidate (wave), resolves (lane)
+  unsigned stats[4] = {0, 0, 0, 0};  // groups, groups with a candidate (wave), resolves (lane), sphere resolves (wave)
 #endif
 
   const SceneView<float> sc{geom, sh0, sh1, a.n};
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
   __builtin_amdgcn_wave_barrier();
   if (lane == 0) atomicAdd(segments, wave_segs[wave]);
 #if RTMI_STATS
-  if (lane == 0) { atomicAdd(&segments[1], (unsigned long long)stats[0]); atomicAdd(&segments[2], (unsigned long long)stats[1]); }
+  if (lane == 0) { atomicAdd(&segments[1], (unsigned long long)stats[0]); atomicAdd(&segments[2], (unsigned long long)stats[1]); atomicAdd(&segments[4], (unsigned long long)stats[3]); }
   atomicAdd(&segments[3], (unsigned long long)stats[2]);
 #endif
   RTMI_TRACE_END(1)
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
   int n_taken = 0;
   RTMI_TRACE_BEGIN
 #if RTMI_STATS
-  unsigned stats[3] = {0, 0, 0};
+  unsigned stats[4] = {0, 0, 0, 0};
 #endif
   const SceneView<float> sc{geom, sh0, sh1, a.n};
 
@@ -478,7 +478,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
   __builtin_amdgcn_wave_barrier();
   if (lane == 0) atomicAdd(segments, wave_segs[wave]);
 #if RTMI_STATS
-  if (lane == 0) { atomicAdd(&segments[1], (unsigned long long)stats[0]); atomicAdd(&segments[2], (unsigned long long)stats[1]); }
+  if (lane == 0) { atomicAdd(&segments[1], (unsigned long long)stats[0]); atomicAdd(&segments[2], (unsigned long long)stats[1]); atomicAdd(&segments[4], (unsigned long long)stats[3]); }
   atomicAdd(&segments[3], (unsigned long long)stats[2]);
 #endif
   RTMI_TRACE_END(n_taken)
@@ -666,8 +666,8 @@ RTMI_EXPORT int rt_ctx_create(int32_t device, rt_ctx **out) {
   auto ctx = std::make_unique<rt_ctx>();
   ctx->device = device;
   HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-  if (int rc = dev_alloc(&ctx->segments, 4)) return rc;
-  HIP_TRY(hipMemset(ctx->segments, 0, 4 * sizeof(unsigned long long)));
+  if (int rc = dev_alloc(&ctx->segments, 8)) return rc;
+  HIP_TRY(hipMemset(ctx->segments, 0, 8 * sizeof(unsigned long long)));
   if (int rc = dev_alloc(&ctx->counter, 1)) return rc;
   {
     // resident blocks per CU for the persistent grid; over-subscription is
@@ -806,7 +806,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
                      uint64_t seed, int32_t row0, int32_t row_step, int32_t nrows, float *strip, hipStream_t st) {
   const size_t n_out = size_t(nrows) * size_t(W) * 3;
   ctx->last_stream = st;
-  HIP_TRY(hipMemsetAsync(ctx->segments, 0, 4 * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(ctx->segments, 0, 8 * sizeof(unsigned long long), st));
   if (nrows == 0) return RT_OK;
   // valid rows: row0 + r*row_step < H
   int32_t nvalid = 0;
@@ -1008,7 +1008,8 @@ RTMI_EXPORT int rt_ctx_last_segments(rt_ctx *ctx, uint64_t *segments) {
 
 // Debug counters of the last render (RTMI_STATS builds only; zeros otherwise):
 // out[0] = world.hit calls, out[1] = sphere groups tested (per wave),
-// out[2] = groups where some lane had a candidate, out[3] = candidate resolves.
+// out[2] = groups where some lane had a candidate, out[3] = candidate resolves
+// (lane), out[4] = candidate spheres resolved (wave); out has 8 slots.
 // Per-wave trace of the renders since the last call (RTMI_TRACE builds; 0
 // lines otherwise): 4 u64 per wave, see RTMI_TRACE_END.  Returns the count.
 RTMI_EXPORT int rt_ctx_debug_trace(rt_ctx *ctx, uint64_t *out, int32_t cap) {
@@ -1033,9 +1034,9 @@ RTMI_EXPORT int rt_ctx_debug_counters(rt_ctx *ctx, uint64_t *out) {
   if (!ctx || !out) return set_error(RT_EINVAL, "null argument");
   DeviceGuard guard(ctx->device);
   hipStream_t st = ctx->last_stream ? ctx->last_stream : ctx->stream;
-  unsigned long long v[4] = {0, 0, 0, 0};
+  unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   HIP_TRY(hipMemcpyAsync(v, ctx->segments, sizeof v, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  for (int i = 0; i < 4; i++) out[i] = v[i];
+  for (int i = 0; i < 8; i++) out[i] = v[i];
   return RT_OK;
 }

@@ -436,6 +436,9 @@ __device__ __forceinline__ int32_t hit_world_packed(const SpherePair *__restrict
   float t_max = INFINITY;
   int32_t best = -1;
   auto resolve = [&](int32_t idx, float hb, float disc) {
+#if RTMI_STATS
+    stats[2] += 1;
+#endif
     const float sq = dsqrt(disc);
     float root = (-hb - sq) * inv_a;
     bool ok = !(root < t_min || t_max < root);
@@ -497,6 +500,8 @@ __device__ __forceinline__ int32_t hit_world_packed(const SpherePair *__restrict
 #if RTMI_STATS
     stats[0] += 1;
     if (__ballot(any < 0)) stats[1] += 1;
+    for (int k = 0; k < 2 * GP; ++k)
+      if (__ballot(ci[k] < 0)) stats[3] += 1;
 #endif
     if (any < 0) {
 #pragma unroll

@@ -11,9 +11,12 @@ L = rt.load()
 L.rt_ctx_debug_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
 r = rt.Renderer(rt.random_scene(), 0)
 r.render(rt.final_camera(1.5), 1200, 800, 500, 50, 1984)
-v = (C.c_uint64 * 4)()
+v = (C.c_uint64 * 8)()
 L.rt_ctx_debug_counters(r._h, v)
-segs, groups, any_groups, resolves = list(v)
+segs, groups, any_groups, resolves, wave_sph = list(v)[:5]
+wseg = groups / 61
+print(f"per wave-segment: groups-with-candidate {any_groups / wseg:.2f}, spheres resolved (wave) {wave_sph / wseg:.2f}, "
+      f"lane resolves per lane-segment {resolves / segs:.2f}")
 print(f"segments {segs} groups {groups} groups_with_candidate {any_groups} ({any_groups / groups:.3f}) "
       f"lane_resolves {resolves} (per lane-segment {resolves / segs:.2f}; per sphere-test {resolves / (segs * 487):.4f}); "
-      f"wave-iterations {groups / 121:.4g}; lane utilisation {segs / (groups / 121 * 64):.3f}")
+      f"wave-segments {wseg:.4g}; lane utilisation {segs / (wseg * 64):.3f}")

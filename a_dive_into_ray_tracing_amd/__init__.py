@@ -22,6 +22,7 @@ from ._abi import RT_MAT_DIELECTRIC, RT_MAT_LAMBERTIAN, RT_MAT_METAL, RtCamera, 
 __all__ = [
     "RTError", "World", "lambertian", "metal", "dielectric", "sphere", "random_scene", "learn_scene",
     "camera", "final_camera", "learn_camera", "Renderer", "render", "quantize", "write_ppm", "device_count",
+    "write_pfm", "read_pfm", "load_scene",
 ]
 
 _dp = C.POINTER(C.c_double)
@@ -73,6 +74,20 @@ class World:
     def __len__(self):
         return int(self.mat_kind.size)
 
+    def save(self, path):
+        """Scene text file (rt_scene_write; the format of tests/golden/scene_final.txt)."""
+        sc = self.c_struct()
+        check(load().rt_scene_write(str(path).encode(), C.byref(sc)), "rt_scene_write")
+
+    def digest(self):
+        """sha256 of the scene arrays (checkpoint headers)."""
+        import hashlib
+
+        h = hashlib.sha256()
+        for a in (self.center_radius, self.mat_kind, self.mat_params):
+            h.update(np.ascontiguousarray(a).tobytes())
+        return h.hexdigest()
+
     def c_struct(self):
         self._keep = [np.ascontiguousarray(self.center_radius), np.ascontiguousarray(self.mat_kind), np.ascontiguousarray(self.mat_params)]
         g, k, m = self._keep
@@ -86,6 +101,19 @@ def random_scene(glibc_seed=1):
     k = np.zeros(1024, np.int32)
     n = C.c_int32()
     check(L.rt_scene_random(glibc_seed, _d(g), k.ctypes.data_as(_ip), _d(m), 1024, C.byref(n)), "rt_scene_random")
+    return World(g[: 4 * n.value], k[: n.value], m[: 4 * n.value])
+
+
+def load_scene(path):
+    """Scene text file -> World (rt_scene_read)."""
+    L = load()
+    n = C.c_int32()
+    rc = L.rt_scene_read(str(path).encode(), None, None, None, 0, C.byref(n))
+    if rc != 0 and n.value == 0:
+        check(rc, "rt_scene_read")
+    g, m = np.zeros(4 * max(n.value, 1)), np.zeros(4 * max(n.value, 1))
+    k = np.zeros(max(n.value, 1), np.int32)
+    check(L.rt_scene_read(str(path).encode(), _d(g), k.ctypes.data_as(_ip), _d(m), n.value, C.byref(n)), "rt_scene_read")
     return World(g[: 4 * n.value], k[: n.value], m[: 4 * n.value])
 
 
@@ -141,6 +169,7 @@ class Renderer:
     def set_scene(self, world):
         sc = world.c_struct()
         check(self.L.rt_ctx_set_scene(self._h, C.byref(sc)), "rt_ctx_set_scene")
+        self.world = world
 
     def set_tuning(self, tile_w=8, chunk=0):
         check(self.L.rt_ctx_set_tuning(self._h, tile_w, chunk), "rt_ctx_set_tuning")
@@ -152,6 +181,17 @@ class Renderer:
 
     def set_kernel(self, kind="auto"):
         check(self.L.rt_ctx_set_kernel(self._h, self.KERNELS[kind]), "rt_ctx_set_kernel")
+
+    ACCELS = {"none": 0, "bvh": 1}  # RT_ACCEL_* (include/rtmi.h)
+
+    def set_accel(self, accel="none"):
+        check(self.L.rt_ctx_set_accel(self._h, self.ACCELS[accel]), "rt_ctx_set_accel")
+
+    def accel_info(self):
+        """(big spheres tested brute force, BVH nodes) for the current scene."""
+        nb, nn = C.c_int32(), C.c_int32()
+        check(self.L.rt_ctx_accel_info(self._h, C.byref(nb), C.byref(nn)), "rt_ctx_accel_info")
+        return nb.value, nn.value
 
     def render(self, cam, W, H, spp, max_depth=50, seed=1984):
         """Whole image, host float32 sums [H, W, 3], row 0 = bottom (main.cpp:274)."""
@@ -193,6 +233,64 @@ class Renderer:
             "rt_replay_worker",
         )
         return out[:total], used
+
+    # ---- progressive accumulation (rt_accum_* / rt_render_pass) ----------
+    def accum_reset(self, W, nrows):
+        check(self.L.rt_accum_reset(self._h, W, nrows), "rt_accum_reset")
+        self._acc_shape = (nrows, W, 3)
+
+    def render_pass(self, cam, W, H, s_begin, s_count, max_depth=50, seed=1984, row0=0, row_step=1, nrows=None, stream=0):
+        """Add samples [s_begin, s_begin + s_count) of the rows to the accumulator (async)."""
+        nrows = H if nrows is None else nrows
+        check(
+            self.L.rt_render_pass(self._h, C.byref(cam), W, H, s_begin, s_count, max_depth, seed, row0, row_step, nrows, C.c_void_p(stream)),
+            "rt_render_pass",
+        )
+
+    def accum_resolve(self):
+        """Float sums of the accumulator [nrows, W, 3] (host)."""
+        out = np.zeros(int(np.prod(self._acc_shape)), np.float32)
+        check(self.L.rt_accum_resolve(self._h, None, out.ctypes.data_as(_fp), None), "rt_accum_resolve")
+        return out.reshape(self._acc_shape)
+
+    def accum_export(self):
+        """(raw int64 fixed-point sums [nrows, W, 3], samples accumulated)."""
+        raw = np.zeros(int(np.prod(self._acc_shape)), np.int64)
+        done = C.c_int32()
+        check(self.L.rt_accum_export(self._h, raw.ctypes.data_as(C.POINTER(C.c_int64)), raw.size, C.byref(done)), "rt_accum_export")
+        return raw.reshape(self._acc_shape), done.value
+
+    def accum_import(self, raw, spp_done):
+        raw = np.ascontiguousarray(raw, np.int64)
+        check(self.L.rt_accum_import(self._h, raw.ctypes.data_as(C.POINTER(C.c_int64)), raw.size, spp_done), "rt_accum_import")
+
+    def progressive(self, cam, W, H, spp, pass_spp, max_depth=50, seed=1984, row0=0, row_step=1, nrows=None,
+                    checkpoint=None, on_pass=None):
+        """Samples [0, spp) in passes of pass_spp (each a bounded kernel), resuming
+        from / saving to `checkpoint` after every pass.  Returns the float sums
+        [nrows, W, 3]: bit-identical to render(spp) for any pass split."""
+        import os
+
+        nrows = H if nrows is None else nrows
+        self.accum_reset(W, nrows)
+        sc = self.world.c_struct()
+        done = 0
+        if checkpoint and os.path.exists(checkpoint):
+            n = C.c_int32()
+            check(self.L.rt_accum_load(self._h, str(checkpoint).encode(), C.byref(sc), C.byref(cam), W, H, row0, row_step,
+                                       nrows, max_depth, seed, C.byref(n)), "rt_accum_load")
+            done = n.value
+        while done < spp:
+            k = min(pass_spp, spp - done)
+            self.render_pass(cam, W, H, done, k, max_depth, seed, row0, row_step, nrows)
+            done += k
+            if checkpoint:
+                check(self.L.rt_accum_save(self._h, str(checkpoint).encode(), C.byref(sc), C.byref(cam), H, row0, row_step,
+                                           max_depth, seed), "rt_accum_save")
+            if on_pass is not None:
+                self.synchronize()
+                on_pass(done)
+        return self.accum_resolve()
 
     def close(self):
         if self._h:
@@ -236,3 +334,24 @@ def write_ppm(path, sums, spp, binary=False):
     s = np.ascontiguousarray(sums, np.float32)
     H, W, _ = s.shape
     check(load().rt_write_ppm(path.encode(), s.ctypes.data_as(_fp), W, H, spp, int(binary)), "rt_write_ppm")
+
+
+def write_pfm(path, sums, spp):
+    """PFM of the pre-gamma mean (rt_write_pfm): bottom row first, little-endian."""
+    s = np.ascontiguousarray(sums, np.float32)
+    H, W, _ = s.shape
+    check(load().rt_write_pfm(str(path).encode(), s.ctypes.data_as(_fp), W, H, spp), "rt_write_pfm")
+
+
+def read_pfm(path):
+    """PFM -> float32 [H, W, 3] in file row order (bottom row first), no GPU or library needed."""
+    with open(path, "rb") as f:
+        tag = f.readline().strip()
+        if tag != b"PF":
+            raise ValueError(f"{path}: not a colour PFM ({tag!r})")
+        W, H = (int(x) for x in f.readline().split())
+        scale = float(f.readline())
+        data = np.frombuffer(f.read(), dtype="<f4" if scale < 0 else ">f4")
+    if data.size != W * H * 3:
+        raise ValueError(f"{path}: {data.size} floats for {W}x{H}")
+    return data.reshape(H, W, 3).astype(np.float32)

@@ -54,6 +54,9 @@ SIGNATURES = {
     "rt_scene_learn": (C.c_int, [_dp, _ip, _dp, C.c_int32, _ip]),
     "rt_write_ppm": (C.c_int, [C.c_char_p, _fp, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "rt_quantize": (C.c_int, [_fp, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]),
+    "rt_write_pfm": (C.c_int, [C.c_char_p, _fp, C.c_int32, C.c_int32, C.c_int32]),
+    "rt_scene_write": (C.c_int, [C.c_char_p, C.POINTER(RtScene)]),
+    "rt_scene_read": (C.c_int, [C.c_char_p, _dp, _ip, _dp, C.c_int32, _ip]),
     "rt_device_count": (C.c_int, [_ip]),
     "rt_ctx_create": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
     "rt_ctx_destroy": (C.c_int, [C.c_void_p]),
@@ -61,6 +64,8 @@ SIGNATURES = {
     "rt_ctx_set_tuning": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "rt_ctx_set_schedule": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
     "rt_ctx_set_kernel": (C.c_int, [C.c_void_p, C.c_int32]),
+    "rt_ctx_set_accel": (C.c_int, [C.c_void_p, C.c_int32]),
+    "rt_ctx_accel_info": (C.c_int, [C.c_void_p, _ip, _ip]),
     "rt_render": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_uint64, _fp]),
     "rt_render_rows": (
         C.c_int,
@@ -68,6 +73,19 @@ SIGNATURES = {
     ),
     "rt_ctx_synchronize": (C.c_int, [C.c_void_p]),
     "rt_ctx_last_segments": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    "rt_accum_reset": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    "rt_render_pass": (
+        C.c_int,
+        [C.c_void_p, C.POINTER(RtCamera)] + [C.c_int32] * 5 + [C.c_uint64] + [C.c_int32] * 3 + [C.c_void_p],
+    ),
+    "rt_accum_resolve": (C.c_int, [C.c_void_p, C.c_void_p, _fp, C.c_void_p]),
+    "rt_accum_export": (C.c_int, [C.c_void_p, _lp, C.c_size_t, _ip]),
+    "rt_accum_import": (C.c_int, [C.c_void_p, _lp, C.c_size_t, C.c_int32]),
+    "rt_accum_save": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(RtScene), C.POINTER(RtCamera)] + [C.c_int32] * 4 + [C.c_uint64]),
+    "rt_accum_load": (
+        C.c_int,
+        [C.c_void_p, C.c_char_p, C.POINTER(RtScene), C.POINTER(RtCamera)] + [C.c_int32] * 6 + [C.c_uint64, _ip],
+    ),
     "rt_replay_worker": (C.c_int, [C.c_void_p, C.POINTER(RtCamera)] + [C.c_int32] * 5 + [_ip, _ip, _lp, _dp, _lp]),
     "rt_render_multi": (C.c_int, [C.POINTER(RtScene), C.POINTER(RtCamera)] + [C.c_int32] * 4 + [C.c_uint64, C.c_int32, _fp]),
 }

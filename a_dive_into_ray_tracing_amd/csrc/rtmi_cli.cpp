@@ -5,12 +5,19 @@
 //
 //   rtmi_render [--scene final|learn] [--width W] [--height H] [--spp S]
 //               [--depth D] [--seed N] [--gpus G] [--out FILE|-] [--p6]
-//               [--tile-w 8|16|32|64] [--chunk N]
+//               [--tile-w 8|16|32|64] [--chunk N] [--scene-file F]
+//               [--save-scene F] [--pfm F] [--pass-spp N [--checkpoint F]]
 //
 // --gpus 1 uses rt_render on device 0; --gpus G>1 (or 0 = all) uses
-// rt_render_multi (interleaved rows + one RCCL gather).  Timing goes to
+// rt_render_multi (interleaved rows + one RCCL gather).  --pass-spp renders
+// progressively on device 0 (rt_render_pass, bounded kernels) and, with
+// --checkpoint, saves the accumulator after every pass and resumes from it
+// (SURVEY §8(f) rank 2).  --scene-file reads a scene text file instead of
+// generating one (rt_scene_read), --save-scene writes the scene used,
+// --pfm writes the pre-gamma mean as PFM next to the PPM.  Timing goes to
 // stderr as one JSON line (wall clock, unlike the reference's clock(), which
 // sums CPU time over threads: main.cpp:323-342).
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -27,8 +34,8 @@ static int die(const char *what, int rc) {
 }
 
 int main(int argc, char **argv) {
-  std::string scene = "final", out = "-";
-  int W = 1200, H = -1, spp = 500, depth = 50, gpus = 1, p6 = 0, tile_w = 8, chunk = 0;
+  std::string scene = "final", out = "-", scene_file, save_scene, pfm, checkpoint;
+  int W = 1200, H = -1, spp = 500, depth = 50, gpus = 1, p6 = 0, tile_w = 8, chunk = 0, pass_spp = 0;
   unsigned long long seed = 1984;
   for (int a = 1; a < argc; a++) {
     auto need = [&](const char *f) -> const char * {
@@ -46,9 +53,16 @@ int main(int argc, char **argv) {
     else if (!std::strcmp(argv[a], "--tile-w")) tile_w = std::atoi(need("--tile-w"));
     else if (!std::strcmp(argv[a], "--chunk")) chunk = std::atoi(need("--chunk"));
     else if (!std::strcmp(argv[a], "--p6")) p6 = 1;
+    else if (!std::strcmp(argv[a], "--scene-file")) scene_file = need("--scene-file");
+    else if (!std::strcmp(argv[a], "--save-scene")) save_scene = need("--save-scene");
+    else if (!std::strcmp(argv[a], "--pfm")) pfm = need("--pfm");
+    else if (!std::strcmp(argv[a], "--pass-spp")) pass_spp = std::atoi(need("--pass-spp"));
+    else if (!std::strcmp(argv[a], "--checkpoint")) checkpoint = need("--checkpoint");
     else {
       std::fprintf(stderr, "usage: %s [--scene final|learn] [--width W] [--height H] [--spp S] [--depth D]\n"
-                           "          [--seed N] [--gpus G] [--out FILE|-] [--p6] [--tile-w T] [--chunk N]\n", argv[0]);
+                           "          [--seed N] [--gpus G] [--out FILE|-] [--p6] [--tile-w T] [--chunk N]\n"
+                           "          [--scene-file F] [--save-scene F] [--pfm F] [--pass-spp N [--checkpoint F]]\n",
+                   argv[0]);
       return 2;
     }
   }
@@ -59,13 +73,20 @@ int main(int argc, char **argv) {
   if (H < 0) H = static_cast<int>(W / aspect);                    // main.cpp:188 / :296
   if (learn && spp == 500) spp = 100;                             // main.cpp:189
 
-  std::vector<double> geom(4 * 600), mat(4 * 600);
-  std::vector<int32_t> kind(600);
+  if (!checkpoint.empty() && pass_spp <= 0) { std::fprintf(stderr, "--checkpoint needs --pass-spp\n"); return 2; }
   int32_t n = 0;
-  int rc = learn ? rt_scene_learn(geom.data(), kind.data(), mat.data(), 600, &n)
-                 : rt_scene_random(1, geom.data(), kind.data(), mat.data(), 600, &n);
+  int rc = 0;
+  if (!scene_file.empty() && (rc = rt_scene_read(scene_file.c_str(), nullptr, nullptr, nullptr, 0, &n)) && n == 0)
+    return die("rt_scene_read", rc);
+  const int32_t cap = scene_file.empty() ? 600 : n;
+  std::vector<double> geom(4 * size_t(cap)), mat(4 * size_t(cap));
+  std::vector<int32_t> kind(cap);
+  if (!scene_file.empty()) rc = rt_scene_read(scene_file.c_str(), geom.data(), kind.data(), mat.data(), cap, &n);
+  else if (learn) rc = rt_scene_learn(geom.data(), kind.data(), mat.data(), cap, &n);
+  else rc = rt_scene_random(1, geom.data(), kind.data(), mat.data(), cap, &n);
   if (rc) return die("scene", rc);
   rt_scene sc{n, geom.data(), kind.data(), mat.data()};
+  if (!save_scene.empty() && (rc = rt_scene_write(save_scene.c_str(), &sc))) return die("rt_scene_write", rc);
 
   rt_camera cam;
   const double vup[3] = {0, 1, 0};
@@ -81,7 +102,36 @@ int main(int argc, char **argv) {
 
   std::vector<float> sum(size_t(W) * H * 3);
   double seconds = 0;
-  if (gpus == 1) {
+  int spp_resumed = 0;
+  if (pass_spp > 0) {
+    rt_ctx *ctx = nullptr;
+    if ((rc = rt_ctx_create(0, &ctx))) return die("rt_ctx_create", rc);
+    if ((rc = rt_ctx_set_scene(ctx, &sc))) return die("rt_ctx_set_scene", rc);
+    if ((rc = rt_ctx_set_tuning(ctx, tile_w, chunk))) return die("rt_ctx_set_tuning", rc);
+    if ((rc = rt_accum_reset(ctx, W, H))) return die("rt_accum_reset", rc);
+    int done = 0;
+    if (!checkpoint.empty()) {
+      if (FILE *probe = std::fopen(checkpoint.c_str(), "rb")) {
+        std::fclose(probe);
+        if ((rc = rt_accum_load(ctx, checkpoint.c_str(), &sc, &cam, W, H, 0, 1, H, depth, seed, &done)))
+          return die("rt_accum_load", rc);
+        spp_resumed = done;
+      }
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    while (done < spp) {
+      const int k = std::min(pass_spp, spp - done);
+      if ((rc = rt_render_pass(ctx, &cam, W, H, done, k, depth, seed, 0, 1, H, nullptr))) return die("rt_render_pass", rc);
+      done += k;
+      if (!checkpoint.empty() && (rc = rt_accum_save(ctx, checkpoint.c_str(), &sc, &cam, H, 0, 1, depth, seed)))
+        return die("rt_accum_save", rc);
+      if ((rc = rt_ctx_synchronize(ctx))) return die("rt_ctx_synchronize", rc);
+      std::fprintf(stderr, "{\"pass_done_spp\": %d}\n", done);
+    }
+    if ((rc = rt_accum_resolve(ctx, nullptr, sum.data(), nullptr))) return die("rt_accum_resolve", rc);
+    seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    rt_ctx_destroy(ctx);
+  } else if (gpus == 1) {
     rt_ctx *ctx = nullptr;
     if ((rc = rt_ctx_create(0, &ctx))) return die("rt_ctx_create", rc);
     if ((rc = rt_ctx_set_scene(ctx, &sc))) return die("rt_ctx_set_scene", rc);
@@ -98,7 +148,8 @@ int main(int argc, char **argv) {
   std::fprintf(stderr,
                "{\"scene\": \"%s\", \"width\": %d, \"height\": %d, \"spp\": %d, \"depth\": %d, \"gpus\": %d, "
                "\"seconds\": %.6f, \"msamples_per_s\": %.3f}\n",
-               scene.c_str(), W, H, spp, depth, gpus, seconds, double(W) * H * spp / seconds / 1e6);
+               scene.c_str(), W, H, spp, depth, gpus, seconds, double(W) * H * (spp - spp_resumed) / seconds / 1e6);
   if ((rc = rt_write_ppm(out.c_str(), sum.data(), W, H, spp, p6))) return die("rt_write_ppm", rc);
+  if (!pfm.empty() && (rc = rt_write_pfm(pfm.c_str(), sum.data(), W, H, spp))) return die("rt_write_pfm", rc);
   return 0;
 }

@@ -29,11 +29,14 @@
 // bit-for-bit given its rand() stream (rt_replay_worker).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "rtmi_internal.h"
@@ -55,6 +58,10 @@ struct RenderArgs {
   // chunks of chunk1, phase 2 = [spp1, spp) in chunks of chunk2; phase-2 items
   // come last in the grid, so the dispatch tail is one short item
   int32_t tiles, spp1, chunk1, nch1, chunk2, nch2;
+  // progressive passes: this launch renders samples s_base + [0, spp)
+  int32_t s_base;
+  uint64_t out_elems;  // elements of accum / out (RTMI_CHECK builds verify every write)
+  Accel acc;           // BVH kernels only
 };
 
 #ifndef RTMI_WAVES_PER_BLOCK
@@ -73,9 +80,14 @@ constexpr int kWavesPerBlock = RTMI_WAVES_PER_BLOCK;
 constexpr unsigned kTraceCap = 1u << 18;
 __device__ unsigned long long g_trace[kTraceCap * 4];
 __device__ unsigned g_trace_n;
-#define RTMI_TRACE_BEGIN const unsigned long long trace_t0 = __builtin_amdgcn_s_memrealtime();
+#define RTMI_TRACE_BEGIN                                                                 \
+  const unsigned long long trace_t0 = __builtin_amdgcn_s_memrealtime();                  \
+  const unsigned long long cyc_start = __builtin_amdgcn_s_memtime();                     \
+  unsigned long long cyc_hit = 0;
 #define RTMI_TRACE_END(items)                                                            \
   if (lane == 0) {                                                                       \
+    atomicAdd(&segments[5], cyc_hit);                                                    \
+    atomicAdd(&segments[6], __builtin_amdgcn_s_memtime() - cyc_start);                   \
     const unsigned k_ = atomicAdd(&g_trace_n, 1u);                                       \
     if (k_ < kTraceCap) {                                                                \
       g_trace[4 * k_] = trace_t0;                                                        \
@@ -94,6 +106,11 @@ __device__ unsigned g_trace_n;
 #ifndef RTMI_FAIR
 #define RTMI_FAIR 3
 #endif
+// RTMI_CHECK builds (analysis only) bounds-check every accumulator write and
+// count violations in segments[5..7] instead of performing them.
+#ifndef RTMI_CHECK
+#define RTMI_CHECK 0
+#endif
 #ifndef RTMI_FAIR_TIME
 #define RTMI_FAIR_TIME 0
 #endif
@@ -108,7 +125,7 @@ constexpr int kPairGroup = RTMI_PAIR_GROUP;  // sphere pairs per scalar-load gro
 __device__ __forceinline__ int64_t to_fixed(float c) { return int64_t(c * 4294967296.0f); }
 __device__ __forceinline__ float from_fixed(int64_t v) { return float(v) * 0x1p-32f; }
 
-template <int TW, bool CHUNKED>
+template <int TW, bool CHUNKED, bool BVH>
 __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render_kernel(
     const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1,
     const SpherePair *__restrict__ pairs, RenderArgs a, unsigned long long *__restrict__ accum,
@@ -162,7 +179,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
     const int ly = px / vw, lx = px - ly * vw;
     const int i = x0 + lx;
     const int j = a.row0 + (y0 + ly) * a.row_step;
-    rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(s));
+    rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(a.s_base + s));
     const float u = (float(i) + rng.uni()) / float(a.W - 1);  // main.cpp:278
     const float v = (float(j) + rng.uni()) / float(a.H - 1);  // main.cpp:279
     get_ray<true, float>(a.cam, u, v, rng, o, d);
@@ -181,12 +198,26 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
     if (active) {
       float t;
       ++nseg;
-      const int k = hit_world_packed<kPairGroup>(pairs, a.npairs, o, d, t
-#if RTMI_STATS
-                                                 , stats
+#if RTMI_TRACE
+      const unsigned long long cyc0 = __builtin_amdgcn_s_memtime();
 #endif
-      );
-      if (k < 0) {
+      int k;
+      if constexpr (BVH) {
+        k = hit_world_bvh<kPairGroup>(a.acc, o, d, t);
+      } else {
+        k = hit_world_packed<kPairGroup>(pairs, a.npairs, o, d, t
+#if RTMI_STATS
+                                         , stats
+#endif
+        );
+      }
+#if RTMI_TRACE
+      cyc_hit += __builtin_amdgcn_s_memtime() - cyc0;
+#endif
+#if RTMI_CHECK
+      if (k >= a.n) atomicAdd(&segments[7], 1ull << 32);
+#endif
+      if (k < 0 || (RTMI_CHECK && k >= a.n)) {
         const V3<float> sk = sky<true, float>(d);
         col = mk(T.x * sk.x, T.y * sk.y, T.z * sk.z);
         done = true;
@@ -240,6 +271,12 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
   if (lane < nv) {
     const int ly = lane / vw, lx = lane - ly * vw;
     const size_t o3 = (size_t(y0 + ly) * size_t(a.W) + size_t(x0 + lx)) * 3;
+#if RTMI_CHECK
+    if (o3 + 3 > a.out_elems) {
+      atomicAdd(&segments[5], 1ull);
+      atomicMax(&segments[6], (unsigned long long)o3);
+    } else
+#endif
     for (int c = 0; c < 3; ++c) {
       const unsigned long long v = acc[wave][c][lane];
       if constexpr (CHUNKED) atomicAdd(&accum[o3 + c], v);
@@ -289,7 +326,7 @@ __device__ __forceinline__ ItemDesc describe_item(const RenderArgs &a, int item)
   return r;
 }
 
-template <int TW, bool CHUNKED>
+template <int TW, bool CHUNKED, bool BVH>
 __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void render_persistent(
     const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1,
     const SpherePair *__restrict__ pairs, RenderArgs a, unsigned long long *__restrict__ accum,
@@ -339,6 +376,12 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
     if (lane < it.nv) {
       const int ly = lane / it.vw, lx = lane - ly * it.vw;
       const size_t o3 = (size_t(it.y0 + ly) * size_t(a.W) + size_t(it.x0 + lx)) * 3;
+#if RTMI_CHECK
+      if (o3 + 3 > a.out_elems || s < 0 || s > 1) {
+        atomicAdd(&segments[5], 1ull);
+        atomicMax(&segments[6], (unsigned long long)o3);
+      } else
+#endif
       for (int c = 0; c < 3; ++c) {
         const unsigned long long v = acc[wave][s][c][lane];
         if constexpr (CHUNKED) atomicAdd(&accum[o3 + c], v);
@@ -364,7 +407,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
           const int ly = px / cd.vw, lx = px - ly * cd.vw;
           const int i = cd.x0 + lx;
           const int j = a.row0 + (cd.y0 + ly) * a.row_step;
-          rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(cd.s0 + qs));
+          rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(a.s_base + cd.s0 + qs));
           const float u = (float(i) + rng.uni()) / float(a.W - 1);  // main.cpp:278
           const float v = (float(j) + rng.uni()) / float(a.H - 1);  // main.cpp:279
           get_ray<true, float>(a.cam, u, v, rng, o, d);
@@ -425,12 +468,26 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
     if (active) {
       float t;
       ++nseg;
-      const int k = hit_world_packed<kPairGroup>(pairs, a.npairs, o, d, t
-#if RTMI_STATS
-                                                 , stats
+#if RTMI_TRACE
+      const unsigned long long cyc0 = __builtin_amdgcn_s_memtime();
 #endif
-      );
-      if (k < 0) {
+      int k;
+      if constexpr (BVH) {
+        k = hit_world_bvh<kPairGroup>(a.acc, o, d, t);
+      } else {
+        k = hit_world_packed<kPairGroup>(pairs, a.npairs, o, d, t
+#if RTMI_STATS
+                                         , stats
+#endif
+        );
+      }
+#if RTMI_TRACE
+      cyc_hit += __builtin_amdgcn_s_memtime() - cyc0;
+#endif
+#if RTMI_CHECK
+      if (k >= a.n) atomicAdd(&segments[7], 1ull << 32);
+#endif
+      if (k < 0 || (RTMI_CHECK && k >= a.n)) {
         const V3<float> sk = sky<true, float>(d);
         col = mk(T.x * sk.x, T.y * sk.y, T.z * sk.z);
         done = true;
@@ -454,6 +511,13 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
       }
     }
     // 3. finished paths add their colour to their item's slot
+#if RTMI_CHECK
+    if (done && (px < 0 || px > 63 || lane_slot < 0 || lane_slot > 1)) {
+      atomicAdd(&segments[7], 1ull);
+      done = false;
+      active = false;
+    }
+#endif
     if (done) {
       atomicAdd(&acc[wave][lane_slot][0][px], (unsigned long long)to_fixed(col.x));
       atomicAdd(&acc[wave][lane_slot][1][px], (unsigned long long)to_fixed(col.y));
@@ -583,7 +647,19 @@ struct rt_ctx {
   unsigned long long *segments = nullptr;  // world.hit calls of the last render
   unsigned *counter = nullptr;             // persistent kernel's work-item counter
   int32_t kernel = RT_KERNEL_AUTO;         // RT_KERNEL_* (rtmi.h)
+  unsigned long long *pass_accum = nullptr;  // progressive accumulator (fixed point)
+  size_t pass_cap = 0;
+  int32_t pass_W = 0, pass_rows = 0, pass_spp = 0;
   int32_t resident_blocks = 0;             // blocks of the persistent grid (from the occupancy query)
+  // BVH, built by rt_ctx_set_scene
+  int32_t accel = RT_ACCEL_NONE;
+  SpherePair *big_pairs = nullptr;
+  int32_t *big_idx = nullptr;
+  int32_t nbig_pairs = 0, nbig = 0;
+  BvhNode *nodes = nullptr;
+  int32_t nnodes = 0;
+  float4 *bvh_sph = nullptr;
+  int32_t *bvh_idx = nullptr;
   hipStream_t last_stream = nullptr;
   int32_t tile_w = 8;
   int32_t chunk = 0;       // phase-1 samples per item (0 = automatic)
@@ -673,7 +749,7 @@ RTMI_EXPORT int rt_ctx_create(int32_t device, rt_ctx **out) {
     // resident blocks per CU for the persistent grid; over-subscription is
     // harmless (extra waves start later and find the counter exhausted)
     int per_cu = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<8, true>,
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<8, true, false>,
                                                          64 * kWavesPerBlock, 0));
     ctx->resident_blocks = std::max(1, per_cu) * prop.multiProcessorCount;
   }
@@ -686,10 +762,93 @@ RTMI_EXPORT int rt_ctx_destroy(rt_ctx *ctx) {
   DeviceGuard guard(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   for (void *p : {(void *)ctx->geom, (void *)ctx->sh0, (void *)ctx->sh1, (void *)ctx->geom64, (void *)ctx->sh064,
-                  (void *)ctx->sh164, (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments, (void *)ctx->pairs, (void *)ctx->counter})
+                  (void *)ctx->sh164, (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments, (void *)ctx->pairs, (void *)ctx->counter, (void *)ctx->pass_accum,
+                  (void *)ctx->big_pairs, (void *)ctx->big_idx, (void *)ctx->nodes, (void *)ctx->bvh_sph, (void *)ctx->bvh_idx})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
+  return RT_OK;
+}
+
+namespace {
+// BVH over the small spheres: median split on the longest centroid axis,
+// leaves of <= kLeafMax spheres, nodes in DFS order with skip links.  Boxes
+// are the spheres' double-precision bounds grown by a margin (1e-3 of the
+// scene scale, ~100x the float error of the sphere test at that scale) and
+// rounded outward to float, so every sphere the float test can report lies
+// strictly inside its leaf's box.
+struct BvhBuilder {
+  const double *cr;
+  const std::vector<float4> &g;
+  double margin;
+  std::vector<BvhNode> nodes;
+  std::vector<float4> sph;
+  std::vector<int32_t> idx;
+
+  void bounds(const int32_t *ids, int cnt, double lo[3], double hi[3]) const {
+    for (int a = 0; a < 3; ++a) { lo[a] = INFINITY; hi[a] = -INFINITY; }
+    for (int i = 0; i < cnt; ++i) {
+      const double *c = cr + 4 * ids[i];
+      const double rr = std::fabs(c[3]) + margin;
+      for (int a = 0; a < 3; ++a) {
+        lo[a] = std::min(lo[a], c[a] - rr);
+        hi[a] = std::max(hi[a], c[a] + rr);
+      }
+    }
+  }
+  void build(int32_t *ids, int cnt) {
+    const int me = int(nodes.size());
+    nodes.push_back(BvhNode{});
+    double lo[3], hi[3];
+    bounds(ids, cnt, lo, hi);
+    BvhNode nd{};
+    for (int a = 0; a < 3; ++a) {
+      nd.bmin[a] = std::nextafter(float(lo[a]), -INFINITY);
+      nd.bmax[a] = std::nextafter(float(hi[a]), INFINITY);
+    }
+    if (cnt <= kLeafMax) {
+      nd.leaf = (int32_t(sph.size()) << 3) | cnt;
+      for (int i = 0; i < cnt; ++i) {
+        sph.push_back(g[ids[i]]);
+        idx.push_back(ids[i]);
+      }
+      nd.skip = me + 1;
+    } else {
+      double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+      for (int i = 0; i < cnt; ++i)
+        for (int a = 0; a < 3; ++a) {
+          clo[a] = std::min(clo[a], cr[4 * ids[i] + a]);
+          chi[a] = std::max(chi[a], cr[4 * ids[i] + a]);
+        }
+      int ax = 0;
+      for (int a = 1; a < 3; ++a)
+        if (chi[a] - clo[a] > chi[ax] - clo[ax]) ax = a;
+      const int mid = cnt / 2;
+      std::nth_element(ids, ids + mid, ids + cnt, [&](int32_t x, int32_t y) {
+        const double cx = cr[4 * x + ax], cy = cr[4 * y + ax];
+        return cx < cy || (cx == cy && x < y);
+      });
+      build(ids, mid);
+      build(ids + mid, cnt - mid);
+      nd.leaf = -1;
+      nd.skip = int(nodes.size());
+    }
+    nodes[me] = nd;
+  }
+};
+}  // namespace
+
+RTMI_EXPORT int rt_ctx_set_accel(rt_ctx *ctx, int32_t accel) {
+  if (!ctx) return set_error(RT_EINVAL, "null ctx");
+  if (accel != RT_ACCEL_NONE && accel != RT_ACCEL_BVH) return set_error(RT_EINVAL, "unknown accel %d", accel);
+  ctx->accel = accel;
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_ctx_accel_info(rt_ctx *ctx, int32_t *n_big, int32_t *n_nodes) {
+  if (!ctx) return set_error(RT_EINVAL, "null ctx");
+  if (n_big) *n_big = ctx->nbig;
+  if (n_nodes) *n_nodes = ctx->nnodes;
   return RT_OK;
 }
 
@@ -746,6 +905,50 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
   HIP_TRY(hipMemcpy(ctx->geom64, g64.data(), n * sizeof(double4), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(ctx->sh064, s064.data(), n * sizeof(double4), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(ctx->sh164, s164.data(), n * sizeof(double4), hipMemcpyHostToDevice));
+  // BVH: spheres much larger than the typical one (the ground) stay brute force
+  {
+    std::vector<double> rad(n);
+    for (int k = 0; k < n; k++) rad[k] = std::fabs(scene->center_radius[4 * k + 3]);
+    std::vector<double> sorted_r = rad;
+    std::nth_element(sorted_r.begin(), sorted_r.begin() + n / 2, sorted_r.end());
+    const double med = sorted_r[n / 2];
+    std::vector<int32_t> big, small;
+    double scale = 0;
+    for (int k = 0; k < n; k++) {
+      (rad[k] > 4 * med ? big : small).push_back(k);
+      if (rad[k] <= 4 * med)
+        for (int a = 0; a < 3; ++a) scale = std::max(scale, std::fabs(scene->center_radius[4 * k + a]) + rad[k]);
+    }
+    BvhBuilder b{scene->center_radius, g, 1e-3 * (1.0 + scale), {}, {}, {}};
+    if (!small.empty()) b.build(small.data(), int(small.size()));
+    const int nb_pad = big.empty() ? 0 : (int(big.size()) + 2 * kPairGroup - 1) / (2 * kPairGroup) * (2 * kPairGroup);
+    std::vector<SpherePair> bp(nb_pad / 2 + kPairGroup);
+    std::vector<int32_t> bidx(size_t(nb_pad) + 2 * kPairGroup, -1);
+    for (auto &p : bp) {
+      p.cx = f2v{0.f, 0.f}; p.cy = f2v{0.f, 0.f}; p.cz = f2v{0.f, 0.f}; p.S = f2v{kDummyS, kDummyS};
+    }
+    for (size_t s = 0; s < big.size(); s++) {  // ascending scene index
+      SpherePair &p = bp[s / 2];
+      const int h = int(s & 1), k = big[s];
+      p.cx[h] = g[k].x; p.cy[h] = g[k].y; p.cz[h] = g[k].z; p.S[h] = g[k].w;
+      bidx[s] = k;
+    }
+    if ((rc = dev_alloc(&ctx->big_pairs, bp.size())) || (rc = dev_alloc(&ctx->big_idx, bidx.size())) ||
+        (rc = dev_alloc(&ctx->nodes, std::max<size_t>(b.nodes.size(), 1))) ||
+        (rc = dev_alloc(&ctx->bvh_sph, std::max<size_t>(b.sph.size(), 1))) ||
+        (rc = dev_alloc(&ctx->bvh_idx, std::max<size_t>(b.idx.size(), 1))))
+      return rc;
+    HIP_TRY(hipMemcpy(ctx->big_pairs, bp.data(), bp.size() * sizeof(SpherePair), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(ctx->big_idx, bidx.data(), bidx.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    if (!b.nodes.empty()) {
+      HIP_TRY(hipMemcpy(ctx->nodes, b.nodes.data(), b.nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(ctx->bvh_sph, b.sph.data(), b.sph.size() * sizeof(float4), hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(ctx->bvh_idx, b.idx.data(), b.idx.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    }
+    ctx->nbig = int32_t(big.size());
+    ctx->nbig_pairs = nb_pad / 2;
+    ctx->nnodes = int32_t(b.nodes.size());
+  }
   ctx->n = n;
   return RT_OK;
 }
@@ -779,43 +982,58 @@ RTMI_EXPORT int rt_ctx_set_tuning(rt_ctx *ctx, int32_t tile_w, int32_t chunk) {
 
 namespace {
 
-template <int TW>
+template <int TW, bool BVH>
 void launch_persistent(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a,
                        unsigned long long *accum, float *out) {
   if (chunked)
-    hipLaunchKernelGGL((render_persistent<TW, true>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
+    hipLaunchKernelGGL((render_persistent<TW, true, BVH>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
                        ctx->sh1, ctx->pairs, a, accum, out, ctx->segments, ctx->counter);
   else
-    hipLaunchKernelGGL((render_persistent<TW, false>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
-                       ctx->sh1, ctx->pairs, a, accum, out, ctx->segments, ctx->counter);
+    hipLaunchKernelGGL((render_persistent<TW, false, BVH>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom,
+                       ctx->sh0, ctx->sh1, ctx->pairs, a, accum, out, ctx->segments, ctx->counter);
 }
 
-template <int TW>
+template <int TW, bool BVH>
 void launch_tw(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a,
                unsigned long long *accum, float *out) {
   if (chunked)
-    hipLaunchKernelGGL((render_kernel<TW, true>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
+    hipLaunchKernelGGL((render_kernel<TW, true, BVH>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
                        ctx->sh1, ctx->pairs, a, accum, out, ctx->segments);
   else
-    hipLaunchKernelGGL((render_kernel<TW, false>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
+    hipLaunchKernelGGL((render_kernel<TW, false, BVH>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
                        ctx->sh1, ctx->pairs, a, accum, out, ctx->segments);
 }
 
+template <int TW>
+void launch_shape(bool persistent, bool bvh, bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx,
+                  const RenderArgs &a, unsigned long long *accum, float *out) {
+  if (persistent) {
+    if (bvh) launch_persistent<TW, true>(chunked, grid, st, ctx, a, accum, out);
+    else launch_persistent<TW, false>(chunked, grid, st, ctx, a, accum, out);
+  } else {
+    if (bvh) launch_tw<TW, true>(chunked, grid, st, ctx, a, accum, out);
+    else launch_tw<TW, false>(chunked, grid, st, ctx, a, accum, out);
+  }
+}
+
 // The render of one row set into a device strip; all work on `st`.
+// With pass_accum set (a progressive pass), samples s_base + [0, spp) are
+// added to that fixed-point accumulator ([nrows][W][3]) and nothing is
+// written to `strip`.
 int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t spp, int32_t max_depth,
-                     uint64_t seed, int32_t row0, int32_t row_step, int32_t nrows, float *strip, hipStream_t st) {
-  const size_t n_out = size_t(nrows) * size_t(W) * 3;
+                     uint64_t seed, int32_t row0, int32_t row_step, int32_t nrows, float *strip, hipStream_t st,
+                     int32_t s_base = 0, unsigned long long *pass_accum = nullptr) {
   ctx->last_stream = st;
   HIP_TRY(hipMemsetAsync(ctx->segments, 0, 8 * sizeof(unsigned long long), st));
   if (nrows == 0) return RT_OK;
   // valid rows: row0 + r*row_step < H
   int32_t nvalid = 0;
   if (row0 < H) nvalid = std::min<int64_t>(nrows, (int64_t(H) - row0 + row_step - 1) / row_step);
-  if (nvalid < nrows)
+  if (nvalid < nrows && !pass_accum)
     HIP_TRY(hipMemsetAsync(strip + size_t(nvalid) * W * 3, 0, size_t(nrows - nvalid) * W * 3 * sizeof(float), st));
-  if (nvalid == 0) return RT_OK;
+  if (nvalid == 0 || (pass_accum && spp == 0)) return RT_OK;
   if (max_depth == 0) {  // ray_color returns black before any hit test (main.cpp:58-60)
-    HIP_TRY(hipMemsetAsync(strip, 0, size_t(nvalid) * W * 3 * sizeof(float), st));
+    if (!pass_accum) HIP_TRY(hipMemsetAsync(strip, 0, size_t(nvalid) * W * 3 * sizeof(float), st));
     return RT_OK;
   }
   const int TW = ctx->tile_w, TH = 64 / TW;
@@ -863,9 +1081,11 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   a.row0 = row0; a.row_step = row_step; a.nrows_valid = nvalid;
   a.tiles_x = tiles_x; a.n_items = int32_t(items);
   a.tiles = int32_t(tiles); a.spp1 = spp1; a.chunk1 = chunk1; a.nch1 = nch1; a.chunk2 = chunk2; a.nch2 = nch2;
-  const bool chunked = nch1 + nch2 > 1;
+  a.s_base = s_base;
+  a.out_elems = uint64_t(nvalid) * uint64_t(W) * 3;
+  const bool chunked = pass_accum || nch1 + nch2 > 1;
   const size_t n_valid_out = size_t(nvalid) * W * 3;
-  if (chunked) {
+  if (chunked && !pass_accum) {
     if (ctx->accum_cap < n_valid_out) {
       int rc = dev_alloc(&ctx->accum, n_valid_out);
       if (rc) { ctx->accum_cap = 0; return rc; }
@@ -873,33 +1093,43 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     }
     HIP_TRY(hipMemsetAsync(ctx->accum, 0, n_valid_out * sizeof(unsigned long long), st));
   }
+  // (after the allocation above, which may replace ctx->accum)
+  unsigned long long *const accum = pass_accum ? pass_accum : ctx->accum;
+  // host-side check of what the kernels will index: accumulator and output
+  // hold the nvalid rows, every work item lies inside them
+  if (chunked && (!accum || (pass_accum ? ctx->pass_cap : ctx->accum_cap) < n_valid_out))
+    return set_error(RT_EHIP, "internal: accumulator not allocated for %zu elements", n_valid_out);
+  if (!chunked && !strip) return set_error(RT_EHIP, "internal: no output strip");
+  if (int64_t(tiles_y) * TH < nvalid || int64_t(tiles_x) * TW < W || nch1 * int64_t(chunk1) < spp1 ||
+      nch2 * int64_t(chunk2) < spp - spp1)
+    return set_error(RT_EHIP, "internal: work items do not cover the image");
+  const bool bvh = ctx->accel == RT_ACCEL_BVH && ctx->nnodes > 0;
+  if (bvh) {
+    a.acc = Accel{ctx->big_pairs, ctx->big_idx, ctx->nbig_pairs, ctx->nnodes, ctx->nodes, ctx->bvh_sph, ctx->bvh_idx};
+  } else {
+    a.acc = Accel{nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr};
+  }
+  dim3 grid;
   if (persistent) {
     // a resident grid of waves pulling items from a global counter
     HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
     const int64_t waves = std::min<int64_t>(items, int64_t(ctx->resident_blocks) * kWavesPerBlock);
-    const dim3 grid(unsigned((waves + kWavesPerBlock - 1) / kWavesPerBlock));
-    switch (TW) {
-      case 8: launch_persistent<8>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
-      case 16: launch_persistent<16>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
-      case 32: launch_persistent<32>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
-      default: launch_persistent<64>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
-    }
+    grid = dim3(unsigned((waves + kWavesPerBlock - 1) / kWavesPerBlock));
   } else {
-    const dim3 grid(unsigned((items + kWavesPerBlock - 1) / kWavesPerBlock));
-    switch (TW) {
-      case 8: launch_tw<8>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
-      case 16: launch_tw<16>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
-      case 32: launch_tw<32>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
-      default: launch_tw<64>(chunked, grid, st, ctx, a, ctx->accum, strip); break;
-    }
+    grid = dim3(unsigned((items + kWavesPerBlock - 1) / kWavesPerBlock));
+  }
+  switch (TW) {
+    case 8: launch_shape<8>(persistent, bvh, chunked, grid, st, ctx, a, accum, strip); break;
+    case 16: launch_shape<16>(persistent, bvh, chunked, grid, st, ctx, a, accum, strip); break;
+    case 32: launch_shape<32>(persistent, bvh, chunked, grid, st, ctx, a, accum, strip); break;
+    default: launch_shape<64>(persistent, bvh, chunked, grid, st, ctx, a, accum, strip); break;
   }
   HIP_TRY(hipGetLastError());
-  if (chunked) {
+  if (chunked && !pass_accum) {
     hipLaunchKernelGGL(finalize_kernel, dim3(unsigned((n_valid_out + 255) / 256)), dim3(256), 0, st, ctx->accum,
                        strip, n_valid_out);
     HIP_TRY(hipGetLastError());
   }
-  (void)n_out;
   return RT_OK;
 }
 
@@ -915,6 +1145,179 @@ RTMI_EXPORT int rt_render_rows(rt_ctx *ctx, const rt_camera *cam, int32_t W, int
   DeviceGuard guard(ctx->device);
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   return render_rows_impl(ctx, cam, W, H, spp, max_depth, seed, row0, row_step, nrows, dev_strip, st);
+}
+
+// ---------------------------------------------------------------------------
+// progressive accumulation
+// ---------------------------------------------------------------------------
+// The accumulator holds the fixed-point sums (2^-32, int64) of the passes
+// so far; integer addition makes any split of [0, spp) into passes give the
+// same sums, bit for bit, as one rt_render of spp samples.
+RTMI_EXPORT int rt_accum_reset(rt_ctx *ctx, int32_t W, int32_t nrows) {
+  if (!ctx) return set_error(RT_EINVAL, "null ctx");
+  if (W < 1 || nrows < 0) return set_error(RT_EINVAL, "rt_accum_reset: bad size %dx%d", W, nrows);
+  DeviceGuard guard(ctx->device);
+  const size_t n = size_t(W) * size_t(nrows) * 3;
+  if (ctx->pass_cap < n) {
+    int rc = dev_alloc(&ctx->pass_accum, std::max<size_t>(n, 1));
+    if (rc) { ctx->pass_cap = 0; return rc; }
+    ctx->pass_cap = n;
+  }
+  ctx->pass_W = W;
+  ctx->pass_rows = nrows;
+  ctx->pass_spp = 0;
+  if (n) HIP_TRY(hipMemsetAsync(ctx->pass_accum, 0, n * sizeof(unsigned long long), ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_render_pass(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t s_begin,
+                               int32_t s_count, int32_t max_depth, uint64_t seed, int32_t row0, int32_t row_step,
+                               int32_t nrows, void *stream) {
+  int rc = check_render_args(ctx, cam, W, H, std::max(s_count, 1), max_depth);
+  if (rc) return rc;
+  if (s_begin < 0 || s_count < 0 || int64_t(s_begin) + s_count > INT32_MAX)
+    return set_error(RT_EINVAL, "rt_render_pass: bad sample range [%d, +%d)", s_begin, s_count);
+  if (row0 < 0 || row_step < 1 || nrows < 0) return set_error(RT_EINVAL, "rt_render_pass: bad row set");
+  if (!ctx->pass_accum || W != ctx->pass_W || nrows != ctx->pass_rows)
+    return set_error(RT_EINVAL, "rt_render_pass: accumulator is not %dx%d (call rt_accum_reset)", W, nrows);
+  DeviceGuard guard(ctx->device);
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  if ((rc = render_rows_impl(ctx, cam, W, H, s_count, max_depth, seed, row0, row_step, nrows, nullptr, st, s_begin,
+                             ctx->pass_accum)))
+    return rc;
+  ctx->pass_spp += s_count;
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_accum_resolve(rt_ctx *ctx, float *dev_sum, float *host_sum, void *stream) {
+  if (!ctx) return set_error(RT_EINVAL, "null ctx");
+  if (!ctx->pass_accum) return set_error(RT_EINVAL, "rt_accum_resolve: no accumulator");
+  if (!dev_sum && !host_sum) return set_error(RT_EINVAL, "rt_accum_resolve: no output");
+  DeviceGuard guard(ctx->device);
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  const size_t n = size_t(ctx->pass_W) * size_t(ctx->pass_rows) * 3;
+  float *out = dev_sum;
+  if (!out) {
+    if (ctx->scratch_cap < n) {
+      int rc = dev_alloc(&ctx->scratch, n);
+      if (rc) { ctx->scratch_cap = 0; return rc; }
+      ctx->scratch_cap = n;
+    }
+    out = ctx->scratch;
+  }
+  if (n) {
+    hipLaunchKernelGGL(finalize_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, ctx->pass_accum, out, n);
+    HIP_TRY(hipGetLastError());
+  }
+  if (host_sum) {
+    if (n) HIP_TRY(hipMemcpyAsync(host_sum, out, n * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  return RT_OK;
+}
+
+// Checkpoint / resume: the raw fixed-point accumulator (W*nrows*3 int64) and
+// the number of samples it holds.
+RTMI_EXPORT int rt_accum_export(rt_ctx *ctx, int64_t *host, size_t n, int32_t *spp_done) {
+  if (!ctx || !host) return set_error(RT_EINVAL, "null argument");
+  const size_t want = size_t(ctx->pass_W) * size_t(ctx->pass_rows) * 3;
+  if (!ctx->pass_accum || n != want) return set_error(RT_EINVAL, "rt_accum_export: size %zu, accumulator %zu", n, want);
+  DeviceGuard guard(ctx->device);
+  HIP_TRY(hipStreamSynchronize(ctx->last_stream ? ctx->last_stream : ctx->stream));
+  HIP_TRY(hipMemcpy(host, ctx->pass_accum, n * sizeof(int64_t), hipMemcpyDeviceToHost));
+  if (spp_done) *spp_done = ctx->pass_spp;
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_accum_import(rt_ctx *ctx, const int64_t *host, size_t n, int32_t spp_done) {
+  if (!ctx || !host) return set_error(RT_EINVAL, "null argument");
+  const size_t want = size_t(ctx->pass_W) * size_t(ctx->pass_rows) * 3;
+  if (!ctx->pass_accum || n != want)
+    return set_error(RT_EINVAL, "rt_accum_import: size %zu, accumulator %zu (call rt_accum_reset)", n, want);
+  if (spp_done < 0) return set_error(RT_EINVAL, "rt_accum_import: negative sample count");
+  DeviceGuard guard(ctx->device);
+  HIP_TRY(hipMemcpy(ctx->pass_accum, host, n * sizeof(int64_t), hipMemcpyHostToDevice));
+  ctx->pass_spp = spp_done;
+  return RT_OK;
+}
+
+namespace {
+// Checkpoint file (little-endian): "RTMIACC1", int32 W H row0 row_step nrows
+// spp_done max_depth 0, u64 seed, u64 FNV-1a of the scene arrays, u64 FNV-1a
+// of the camera, then the int64 accumulator [nrows][W][3].
+constexpr char kCkptMagic[8] = {'R', 'T', 'M', 'I', 'A', 'C', 'C', '1'};
+struct CkptHeader {
+  char magic[8];
+  int32_t W, H, row0, row_step, nrows, spp_done, max_depth, zero;
+  uint64_t seed, scene_hash, camera_hash;
+};
+static_assert(sizeof(CkptHeader) == 64, "checkpoint header layout");
+
+uint64_t fnv1a(uint64_t h, const void *p, size_t n) {
+  const unsigned char *b = static_cast<const unsigned char *>(p);
+  for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+  return h;
+}
+uint64_t scene_hash(const rt_scene *s) {
+  uint64_t h = 14695981039346656037ull;
+  h = fnv1a(h, &s->n, sizeof s->n);
+  h = fnv1a(h, s->center_radius, sizeof(double) * 4 * size_t(s->n));
+  h = fnv1a(h, s->mat_kind, sizeof(int32_t) * size_t(s->n));
+  return fnv1a(h, s->mat_params, sizeof(double) * 4 * size_t(s->n));
+}
+uint64_t camera_hash(const rt_camera *c) { return fnv1a(14695981039346656037ull, c, sizeof *c); }
+}  // namespace
+
+RTMI_EXPORT int rt_accum_save(rt_ctx *ctx, const char *path, const rt_scene *scene, const rt_camera *cam, int32_t H,
+                              int32_t row0, int32_t row_step, int32_t max_depth, uint64_t seed) {
+  if (!ctx || !path || !scene || !cam) return set_error(RT_EINVAL, "rt_accum_save: null argument");
+  if (!ctx->pass_accum) return set_error(RT_EINVAL, "rt_accum_save: no accumulator");
+  const size_t n = size_t(ctx->pass_W) * size_t(ctx->pass_rows) * 3;
+  std::vector<int64_t> raw(n);
+  int32_t done = 0;
+  if (int rc = rt_accum_export(ctx, raw.data(), n, &done)) return rc;
+  CkptHeader h{};
+  std::memcpy(h.magic, kCkptMagic, 8);
+  h.W = ctx->pass_W; h.H = H; h.row0 = row0; h.row_step = row_step; h.nrows = ctx->pass_rows;
+  h.spp_done = done; h.max_depth = max_depth; h.zero = 0;
+  h.seed = seed; h.scene_hash = scene_hash(scene); h.camera_hash = camera_hash(cam);
+  const std::string tmp = std::string(path) + ".tmp";
+  FILE *f = std::fopen(tmp.c_str(), "wb");
+  if (!f) return set_error(RT_EIO, "rt_accum_save: cannot open %s", tmp.c_str());
+  bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 && std::fwrite(raw.data(), sizeof(int64_t), n, f) == n;
+  if (std::fclose(f) != 0) ok = false;
+  if (!ok || std::rename(tmp.c_str(), path) != 0) return set_error(RT_EIO, "rt_accum_save: write to %s failed", path);
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_accum_load(rt_ctx *ctx, const char *path, const rt_scene *scene, const rt_camera *cam, int32_t W,
+                              int32_t H, int32_t row0, int32_t row_step, int32_t nrows, int32_t max_depth,
+                              uint64_t seed, int32_t *spp_done) {
+  if (!ctx || !path || !scene || !cam || !spp_done) return set_error(RT_EINVAL, "rt_accum_load: null argument");
+  FILE *f = std::fopen(path, "rb");
+  if (!f) return set_error(RT_EIO, "rt_accum_load: cannot open %s", path);
+  CkptHeader h{};
+  const bool hdr = std::fread(&h, sizeof h, 1, f) == 1;
+  if (!hdr || std::memcmp(h.magic, kCkptMagic, 8) != 0) {
+    std::fclose(f);
+    return set_error(RT_EIO, "rt_accum_load: %s is not a checkpoint", path);
+  }
+  if (h.W != W || h.H != H || h.row0 != row0 || h.row_step != row_step || h.nrows != nrows || h.max_depth != max_depth ||
+      h.seed != seed || h.scene_hash != scene_hash(scene) || h.camera_hash != camera_hash(cam)) {
+    std::fclose(f);
+    return set_error(RT_EINVAL, "rt_accum_load: %s was made for another render (size, rows, depth, seed, scene or camera)",
+                     path);
+  }
+  const size_t n = size_t(W) * size_t(nrows) * 3;
+  std::vector<int64_t> raw(n);
+  const bool body = std::fread(raw.data(), sizeof(int64_t), n, f) == n;
+  std::fclose(f);
+  if (!body) return set_error(RT_EIO, "rt_accum_load: %s is truncated", path);
+  if (int rc = rt_accum_reset(ctx, W, nrows)) return rc;
+  if (int rc = rt_accum_import(ctx, raw.data(), n, h.spp_done)) return rc;
+  *spp_done = h.spp_done;
+  return RT_OK;
 }
 
 RTMI_EXPORT int rt_ctx_synchronize(rt_ctx *ctx) {

@@ -227,3 +227,86 @@ RTMI_EXPORT int rt_write_ppm(const char *path, const float *sum, int32_t W, int3
   else if (std::fclose(f) != 0) ok = false;
   return ok ? RT_OK : set_error(RT_EIO, "rt_write_ppm: write to %s failed", path);
 }
+
+// PFM ("PF", 3 channels): the pre-gamma mean sum/spp, little-endian (scale
+// -1), rows bottom to top — the PFM row order is the image's own (row 0 =
+// bottom, main.cpp:274), so rows go out in index order.  SURVEY §8(c) item 5.
+RTMI_EXPORT int rt_write_pfm(const char *path, const float *sum, int32_t W, int32_t H, int32_t spp) {
+  if (!path || !sum || W <= 0 || H <= 0 || spp <= 0) return set_error(RT_EINVAL, "rt_write_pfm: bad argument");
+  FILE *f = std::fopen(path, "wb");
+  if (!f) return set_error(RT_EIO, "rt_write_pfm: cannot open %s: %s", path, std::strerror(errno));
+  bool ok = std::fprintf(f, "PF\n%d %d\n-1.0\n", W, H) > 0;
+  std::vector<float> row(size_t(W) * 3);
+  const float inv = 1.0f / float(spp);
+  for (int32_t j = 0; j < H && ok; ++j) {
+    const float *src = sum + size_t(j) * W * 3;
+    for (size_t k = 0; k < row.size(); ++k) row[k] = src[k] * inv;
+    ok = std::fwrite(row.data(), sizeof(float), row.size(), f) == row.size();
+  }
+  if (std::fclose(f) != 0) ok = false;
+  return ok ? RT_OK : set_error(RT_EIO, "rt_write_pfm: write to %s failed", path);
+}
+
+// Scene text format (tests/golden/scene_final.txt): an optional first line
+// with the sphere count, then one sphere per line
+//   cx cy cz r kind a0 a1 a2 p      (kind RT_MAT_*; p = fuzz | ir; %.17g)
+// '#' starts a comment.  Values are the constructor arguments of
+// sphere(center, r, material) (sphere.h:15-19, material.h), so a double
+// survives the round trip exactly.
+RTMI_EXPORT int rt_scene_write(const char *path, const rt_scene *scene) {
+  if (!path || !scene || scene->n < 0 || (scene->n > 0 && (!scene->center_radius || !scene->mat_kind || !scene->mat_params)))
+    return set_error(RT_EINVAL, "rt_scene_write: bad argument");
+  FILE *f = std::fopen(path, "w");
+  if (!f) return set_error(RT_EIO, "rt_scene_write: cannot open %s: %s", path, std::strerror(errno));
+  bool ok = std::fprintf(f, "%d\n", scene->n) > 0;
+  for (int32_t i = 0; i < scene->n && ok; ++i) {
+    const double *g = scene->center_radius + 4 * i, *m = scene->mat_params + 4 * i;
+    ok = std::fprintf(f, "%.17g %.17g %.17g %.17g %d %.17g %.17g %.17g %.17g\n", g[0], g[1], g[2], g[3],
+                      scene->mat_kind[i], m[0], m[1], m[2], m[3]) > 0;
+  }
+  if (std::fclose(f) != 0) ok = false;
+  return ok ? RT_OK : set_error(RT_EIO, "rt_scene_write: write to %s failed", path);
+}
+
+RTMI_EXPORT int rt_scene_read(const char *path, double *center_radius, int32_t *mat_kind, double *mat_params,
+                              int32_t cap, int32_t *n_out) {
+  if (!path || !n_out || cap < 0 || (cap > 0 && (!center_radius || !mat_kind || !mat_params)))
+    return set_error(RT_EINVAL, "rt_scene_read: bad argument");
+  FILE *f = std::fopen(path, "r");
+  if (!f) return set_error(RT_EIO, "rt_scene_read: cannot open %s: %s", path, std::strerror(errno));
+  SceneWriter w{center_radius, mat_kind, mat_params, cap};
+  char line[1024];
+  int lineno = 0;
+  long declared = -1;
+  int rc = RT_OK;
+  while (std::fgets(line, sizeof line, f)) {
+    ++lineno;
+    if (char *h = std::strchr(line, '#')) *h = 0;
+    double v[9];
+    int kind = 0;
+    const int got = std::sscanf(line, "%lf %lf %lf %lf %d %lf %lf %lf %lf", &v[0], &v[1], &v[2], &v[3], &kind, &v[5],
+                                &v[6], &v[7], &v[8]);
+    if (got <= 0) continue;  // blank / comment
+    if (got == 1 && declared < 0 && w.n == 0 && !w.overflow) {
+      declared = long(v[0]);
+      continue;
+    }
+    if (got != 9) { rc = set_error(RT_EINVAL, "%s:%d: expected 9 fields, got %d", path, lineno, got); break; }
+    if (kind < RT_MAT_LAMBERTIAN || kind > RT_MAT_DIELECTRIC) {
+      rc = set_error(RT_EINVAL, "%s:%d: unknown material kind %d", path, lineno, kind);
+      break;
+    }
+    bool finite = true;
+    for (int k : {0, 1, 2, 3, 5, 6, 7, 8}) finite = finite && std::isfinite(v[k]);
+    if (!finite || v[3] == 0.0) { rc = set_error(RT_EINVAL, "%s:%d: non-finite value or zero radius", path, lineno); break; }
+    w.add(v[0], v[1], v[2], v[3], kind, v[5], v[6], v[7], v[8]);
+    if (w.overflow) ++w.n;  // keep counting for *n_out
+  }
+  std::fclose(f);
+  if (rc) return rc;
+  if (declared >= 0 && declared != w.n)
+    return set_error(RT_EINVAL, "%s: header says %ld spheres, file has %d", path, declared, w.n);
+  *n_out = w.n;
+  if (w.overflow) return set_error(RT_EINVAL, "rt_scene_read: cap %d too small for %d spheres", cap, w.n);
+  return RT_OK;
+}

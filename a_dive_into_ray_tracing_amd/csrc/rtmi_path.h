@@ -515,6 +515,125 @@ __device__ __forceinline__ int32_t hit_world_packed(const SpherePair *__restrict
   return best;
 }
 
+// ---------------------------------------------------------------------------
+// BVH over the small spheres
+// ---------------------------------------------------------------------------
+// Same hit as hit_world_packed, bit for bit: the same expanded per-sphere
+// arithmetic and root logic, and the reference's "later object wins ties"
+// rule made order-independent (a root equal to the current t_max replaces
+// the hit only for a larger sphere index), so the closest hit does not
+// depend on the visiting order.  Boxes are conservative (inflated far beyond
+// float error, rtmi_device.hip build_bvh), so a culled sphere is one the
+// brute-force loop would have rejected.  Large spheres (the R=1000 ground,
+// which bounds everything) stay in a brute-force packed list ("big").
+struct BvhNode {
+  float bmin[3];
+  int32_t skip;  // next node when this subtree is not entered (DFS order; leaf: index + 1)
+  float bmax[3];
+  int32_t leaf;  // -1: inner node (first child = index + 1); else first << 3 | count (1..kLeafMax)
+};
+constexpr int kLeafMax = 4;
+
+struct Accel {
+  const SpherePair *big;     // packed pairs of the big spheres (padded like the scene)
+  const int32_t *big_idx;    // scene index of each big sphere slot (2 per pair)
+  int32_t nbig_pairs;
+  int32_t nnodes;
+  const BvhNode *nodes;
+  const float4 *sph;         // BVH spheres in leaf order: {cx, cy, cz, S}
+  const int32_t *sph_idx;    // their scene indices
+};
+
+template <int GP>
+__device__ __forceinline__ int32_t hit_world_bvh(const Accel &acc_s, V3<float> o, V3<float> d, float &t_hit) {
+  const float a = dot<true>(d, d);
+  const float inv_a = 1.0f / a;
+  const float K = dot<true>(o, d);
+  const float aL = a * dot<true>(o, o);
+  const float n2a = -2.0f * a;
+  const float mx = n2a * o.x, my = n2a * o.y, mz = n2a * o.z;
+  const float t_min = 0.001f;
+  float t_max = INFINITY;
+  int32_t best = -1;
+  // sphere.h:30-38 root logic; tie rule order-independent (see above)
+  auto resolve = [&](int32_t idx, float hb, float disc) {
+    const float sq = dsqrt(disc);
+    float root = (-hb - sq) * inv_a;
+    bool ok = !(root < t_min) && (root < t_max || (root == t_max && idx > best));
+    if (!ok) {
+      root = (-hb + sq) * inv_a;
+      ok = !(root < t_min) && (root < t_max || (root == t_max && idx > best));
+    }
+    if (ok) {
+      t_max = root;
+      best = idx;
+    }
+  };
+  // 1. big spheres: the packed brute-force loop
+  {
+    const f2v DX = {d.x, d.x}, DY = {d.y, d.y}, DZ = {d.z, d.z}, KK = {K, K};
+    const f2v MX = {mx, mx}, MY = {my, my}, MZ = {mz, mz};
+    const f2v AA = {a, a}, AL = {aL, aL};
+    for (int32_t q = 0; q < acc_s.nbig_pairs; q += GP) {
+      SpherePair p[GP];
+#pragma unroll
+      for (int g = 0; g < GP; ++g) p[g] = acc_s.big[q + g];
+      f2v hb[GP], disc[GP];
+      int ci[2 * GP];
+      int any = 0;
+#pragma unroll
+      for (int g = 0; g < GP; ++g) {
+        const f2v hz = __builtin_elementwise_fma(-p[g].cz, DZ, KK);
+        hb[g] = __builtin_elementwise_fma(-p[g].cx, DX, __builtin_elementwise_fma(-p[g].cy, DY, hz));
+        const f2v acc = __builtin_elementwise_fma(MX, p[g].cx, __builtin_elementwise_fma(MY, p[g].cy,
+                        __builtin_elementwise_fma(MZ, p[g].cz, __builtin_elementwise_fma(AA, p[g].S, AL))));
+        disc[g] = __builtin_elementwise_fma(hb[g], hb[g], -acc);
+        ci[2 * g] = ~__float_as_int(disc[g].x);
+        ci[2 * g + 1] = ~__float_as_int(disc[g].y);
+        any |= ci[2 * g] | ci[2 * g + 1];
+      }
+      if (any < 0) {
+#pragma unroll
+        for (int g = 0; g < GP; ++g) {
+          if (ci[2 * g] < 0) resolve(acc_s.big_idx[2 * (q + g)], hb[g].x, disc[g].x);
+          if (ci[2 * g + 1] < 0) resolve(acc_s.big_idx[2 * (q + g) + 1], hb[g].y, disc[g].y);
+        }
+      }
+    }
+  }
+  // 2. the BVH, stackless: per-lane walk of the DFS node array with skip links
+  const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+  int32_t node = 0;
+  while (node < acc_s.nnodes) {
+    const float4 lo = *reinterpret_cast<const float4 *>(&acc_s.nodes[node].bmin[0]);
+    const float4 hi = *reinterpret_cast<const float4 *>(&acc_s.nodes[node].bmax[0]);
+    const float tx0 = (lo.x - o.x) * ix, tx1 = (hi.x - o.x) * ix;
+    const float ty0 = (lo.y - o.y) * iy, ty1 = (hi.y - o.y) * iy;
+    const float tz0 = (lo.z - o.z) * iz, tz1 = (hi.z - o.z) * iz;
+    const float tnear = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx0, tx1), __builtin_fminf(ty0, ty1)),
+                                        __builtin_fminf(tz0, tz1));
+    const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx0, tx1), __builtin_fmaxf(ty0, ty1)),
+                                       __builtin_fmaxf(tz0, tz1));
+    // slack on both ends: the box margin already covers float error; this
+    // keeps ties at the interval ends on the safe side
+    const bool enter = tnear <= tfar * 1.0001f + 1e-6f && tfar >= 0.0f && tnear <= t_max * 1.0001f + 1e-6f;
+    const int32_t leaf = __float_as_int(hi.w);
+    if (enter && leaf >= 0) {
+      const int32_t first = leaf >> 3, cnt = leaf & 7;
+      for (int32_t k = first; k < first + cnt; ++k) {
+        const float4 s = acc_s.sph[k];
+        const float hb = __builtin_fmaf(-s.x, d.x, __builtin_fmaf(-s.y, d.y, __builtin_fmaf(-s.z, d.z, K)));
+        const float acc = __builtin_fmaf(mx, s.x, __builtin_fmaf(my, s.y, __builtin_fmaf(mz, s.z, __builtin_fmaf(a, s.w, aL))));
+        const float disc = __builtin_fmaf(hb, hb, -acc);
+        if (!(disc < 0.0f)) resolve(acc_s.sph_idx[k], hb, disc);
+      }
+    }
+    node = enter ? node + 1 : __float_as_int(lo.w);
+  }
+  t_hit = t_max;
+  return best;
+}
+
 // material::scatter material.h:15-97.  Returns true if the ray scattered.
 template <bool F, class R, class G>
 __device__ __forceinline__ bool scatter(const SceneView<R> &sc, int32_t k, V3<R> din, V3<R> normal,

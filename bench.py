@@ -83,6 +83,7 @@ def main():
     ap.add_argument("--tail-spp", type=int, default=-1)
     ap.add_argument("--tail-chunk", type=int, default=0)
     ap.add_argument("--kernel", choices=["auto", "persistent", "grid"], default="auto")
+    ap.add_argument("--accel", choices=["none", "bvh"], default="none")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--strip-of", type=int, default=0,
                     help="analysis only: time ONE rank's interleaved strip of an N-GPU run on this GPU")
@@ -110,6 +111,7 @@ def main():
     r = rt.Renderer(world, local_rank, tile_w=args.tile_w, chunk=args.chunk)
     r.set_schedule(args.chunk, args.tail_spp, args.tail_chunk)
     r.set_kernel(args.kernel)
+    r.set_accel(args.accel)
     row0, row_step, nrows = rdist.strip_rows(H, rank, N)  # interleaved rows, row j -> rank j % N
     if args.strip_of > 1 and N == 1:  # analysis mode: one rank's share of an N-GPU render
         row0, row_step, nrows = rdist.strip_rows(H, 0, args.strip_of)
@@ -199,6 +201,7 @@ def main():
                 "partition": "interleaved rows, one RCCL gather" if N > 1 else "single GPU",
                 "tile": f"{args.tile_w}x{64 // args.tile_w}",
                 "kernel": args.kernel,
+                "accel": args.accel,
             },
             "roofline": {
                 "bound": "valu",
@@ -212,6 +215,9 @@ def main():
                 "segments_per_sample": round(total_segs / samples, 4),
                 "kernel_ms": round(kernel_ms, 3),
                 "kernel_ms_max_rank": round(kernel_ms_max, 3),
+                # with the BVH the FLOP count stays the brute-force figure
+                # ("work-equivalent"), so frac can pass 1
+                "work_equivalent": args.accel != "none",
             },
             "vs_baseline_ref": "published CPU rt_in_one_weekend 0.1189 Msamples/s (README.md:16-19)",
         }

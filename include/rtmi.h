@@ -101,6 +101,19 @@ int rt_write_ppm(const char *path, const float *sum, int32_t W, int32_t H, int32
 /* Same quantisation into rgb[W*H*3] bytes, top row first. */
 int rt_quantize(const float *sum, int32_t W, int32_t H, int32_t spp, uint8_t *rgb);
 
+/* PFM (colour "PF", little-endian): the pre-gamma mean sum/spp per channel,
+ * bottom row first (PFM's own order, = row index order here). */
+int rt_write_pfm(const char *path, const float *sum, int32_t W, int32_t H, int32_t spp);
+
+/* Scene text files (the format of tests/golden/scene_final.txt): optional
+ * count line, then "cx cy cz r kind a0 a1 a2 p" per sphere (%.17g, kind
+ * RT_MAT_*, p = fuzz | ir), '#' comments.  rt_scene_read fills up to `cap`
+ * spheres and sets *n_out to the file's count (RT_EINVAL if cap is too
+ * small: call with cap 0 to size the arrays). */
+int rt_scene_write(const char *path, const rt_scene *scene);
+int rt_scene_read(const char *path, double *center_radius, int32_t *mat_kind, double *mat_params,
+                  int32_t cap, int32_t *n_out);
+
 /* ---------------- device ----------------------------------------------- */
 int rt_device_count(int32_t *n);
 /* Create a context on HIP device `device` (its own non-blocking stream). */
@@ -126,6 +139,16 @@ int rt_ctx_set_schedule(rt_ctx *ctx, int32_t chunk, int32_t tail_spp, int32_t ta
 enum { RT_KERNEL_GRID = 0, RT_KERNEL_PERSISTENT = 1, RT_KERNEL_AUTO = 2 };
 int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind);
 
+/* Closest-hit search.  RT_ACCEL_NONE: brute force over all spheres, the
+ * reference's hittable_list::hit (hittable_list.h:20-34).  RT_ACCEL_BVH: the
+ * spheres much larger than the median (the ground) brute force, the rest
+ * through a BVH with conservative boxes and an order-independent tie rule:
+ * the same closest hit, bit for bit.  rt_ctx_accel_info
+ * reports the split (big spheres, BVH nodes) of the current scene. */
+enum { RT_ACCEL_NONE = 0, RT_ACCEL_BVH = 1 };
+int rt_ctx_set_accel(rt_ctx *ctx, int32_t accel);
+int rt_ctx_accel_info(rt_ctx *ctx, int32_t *n_big, int32_t *n_nodes);
+
 /* The whole image: replaces the 16-thread worker() block main.cpp:313-338.
  * Synchronous; `sum` is a HOST buffer of W*H*3 floats. */
 int rt_render(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t spp,
@@ -146,6 +169,33 @@ int rt_render_rows(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int3
 int rt_ctx_last_segments(rt_ctx *ctx, uint64_t *segments);
 /* Block until the context's stream is idle. */
 int rt_ctx_synchronize(rt_ctx *ctx);
+
+/* Progressive accumulation (resumable).  The context
+ * keeps a fixed-point accumulator for a W x nrows strip (the rows of
+ * rt_render_rows' row set; nrows = H, row0 0, row_step 1 for a whole image).
+ * rt_render_pass adds samples [s_begin, s_begin + s_count) of every pixel;
+ * any split of [0, S) into passes, in any order, gives bit for bit the sums
+ * of one rt_render(..., spp = S, ...).  rt_accum_resolve converts the sums
+ * to floats into a DEVICE strip and/or a HOST buffer (W*nrows*3).
+ * rt_accum_export / rt_accum_import copy the raw int64 accumulator and its
+ * sample count out / in (checkpoint and resume, across processes). */
+int rt_accum_reset(rt_ctx *ctx, int32_t W, int32_t nrows);
+int rt_render_pass(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t s_begin,
+                   int32_t s_count, int32_t max_depth, uint64_t seed, int32_t row0, int32_t row_step,
+                   int32_t nrows, void *stream);
+int rt_accum_resolve(rt_ctx *ctx, float *dev_sum, float *host_sum, void *stream);
+int rt_accum_export(rt_ctx *ctx, int64_t *host, size_t n, int32_t *spp_done);
+int rt_accum_import(rt_ctx *ctx, const int64_t *host, size_t n, int32_t spp_done);
+/* Checkpoint files: the accumulator plus what it was rendered from (size,
+ * row set, depth, seed, hashes of the scene and camera).  rt_accum_save
+ * writes atomically (tmp + rename); rt_accum_load resets the accumulator to
+ * W x nrows, refuses (RT_EINVAL) a file made for another render, and sets
+ * *spp_done to the samples already in it. */
+int rt_accum_save(rt_ctx *ctx, const char *path, const rt_scene *scene, const rt_camera *cam,
+                  int32_t H, int32_t row0, int32_t row_step, int32_t max_depth, uint64_t seed);
+int rt_accum_load(rt_ctx *ctx, const char *path, const rt_scene *scene, const rt_camera *cam,
+                  int32_t W, int32_t H, int32_t row0, int32_t row_step, int32_t nrows,
+                  int32_t max_depth, uint64_t seed, int32_t *spp_done);
 
 /* Exact replay (validation): runs n_jobs reference worker(start, end, ...)
  * calls (main.cpp:267-290) on the GPU in DOUBLE with the reference's op

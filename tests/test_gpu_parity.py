@@ -271,3 +271,78 @@ def test_segment_count_matches_oracle(final_world, final_renderer):
     cam = rt.final_camera(W / H)
     final_renderer.render(cam, W, H, S, 50, SEED)
     assert final_renderer.last_segments() == O.fast_segments(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
+
+
+# ------------------------------------------------------------ BVH ----------
+@pytest.mark.parametrize("kernel", ["grid", "persistent"])
+def test_bvh_bit_exact_vs_oracle_final(kernel, final_world, final_renderer):
+    """RT_ACCEL_BVH finds the same closest hit as the brute-force loop, so the
+    image equals the (brute-force) oracle bit for bit."""
+    W, H, S = 96, 64, 8
+    cam = rt.final_camera(W / H)
+    nb, nn = final_renderer.accel_info()
+    assert nb == 4 and nn > 100  # ground + the three r=1 spheres stay brute force
+    final_renderer.set_accel("bvh")
+    final_renderer.set_kernel(kernel)
+    try:
+        got = final_renderer.render(cam, W, H, S, 50, SEED)
+        segs = final_renderer.last_segments()
+    finally:
+        final_renderer.set_accel("none")
+        final_renderer.set_kernel("auto")
+    want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
+    assert np.array_equal(got, want), np.abs(got - want).max()
+    assert segs == O.fast_segments(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
+
+
+def test_bvh_learn_scene_edge_cases(learn_renderer):
+    world = rt.learn_scene()
+    for (W, H, S, depth) in [(37, 23, 5, 50), (20, 11, 3, 1), (9, 7, 1, 50)]:
+        cam = rt.learn_camera(W / H)
+        learn_renderer.set_accel("bvh")
+        try:
+            got = learn_renderer.render(cam, W, H, S, depth, SEED)
+        finally:
+            learn_renderer.set_accel("none")
+        want = O.fast_render(o_scene(world), o_cam(cam), W, H, S, depth, SEED)
+        assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_bvh_random_scenes_equal_brute_force(seed):
+    """Random scenes: radii over three decades, overlaps, hollow (negative
+    radius) spheres, huge spheres, coincident centres; BVH == brute force."""
+    g = np.random.default_rng(seed)
+    n = 300
+    c = g.uniform(-8, 8, (n, 3))
+    c[:, 1] = g.uniform(-0.5, 3, n)
+    r = np.exp(g.uniform(np.log(0.01), np.log(1.5), n))
+    r[g.random(n) < 0.05] *= -1  # hollow shells
+    c[10] = c[11]  # coincident pair, equal radii: ties decided by index
+    r[10] = r[11] = 0.3
+    kinds = g.integers(0, 3, n).astype(np.int32)
+    params = np.column_stack([g.uniform(0.1, 0.9, (n, 3)), np.where(kinds == 2, 1.5, g.uniform(0, 0.5, n))])
+    cr = np.column_stack([c, r])
+    cr = np.vstack([[0, -1000, 0, 1000], [0, 1, 40, 30], cr])  # ground + one more big sphere
+    kinds = np.concatenate([[0, 1], kinds]).astype(np.int32)
+    params = np.vstack([[0.5, 0.5, 0.5, 0], [0.7, 0.6, 0.5, 0.1], params])
+    world = rt.World(cr, kinds, params)
+    cam = rt.camera((13, 2, 3), (0, 0, 0), (0, 1, 0), 40.0, 1.5, 0.1, 10.0)
+    r_ = rt.Renderer(world, 0)
+    try:
+        want = r_.render(cam, 72, 48, 6, 50, SEED)
+        r_.set_accel("bvh")
+        got = r_.render(cam, 72, 48, 6, 50, SEED)
+    finally:
+        r_.close()
+    assert np.array_equal(got, want)
+
+
+def test_bvh_config2_equals_brute_force(config2, final_renderer):
+    cam, img = config2
+    final_renderer.set_accel("bvh")
+    try:
+        got = final_renderer.render(cam, 1200, 800, 500, 50, SEED)
+    finally:
+        final_renderer.set_accel("none")
+    assert np.array_equal(got, img)

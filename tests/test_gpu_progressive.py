@@ -1,0 +1,166 @@
+"""Progressive accumulation and config 4 on the GPU.
+
+  * any split of [0, S) into passes gives bit for bit the sums of one
+    render of S samples (the accumulator is integer fixed point);
+  * a checkpoint written after a pass resumes in a fresh context (and
+    through the CLI) to the same image, and a checkpoint made for another
+    render is refused;
+  * config 4 (1200x800, 5000 spp, progressive): the seed-to-seed RMS falls
+    as 1/sqrt(S) over S = 50, 500, 5000, and the 5000-spp image sits closer
+    to the reference's 500-spp gallery image than our own 500-spp image does
+    (the remaining distance is the gallery's own noise).
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import a_dive_into_ray_tracing_amd as rt
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+GOLD = O.GOLDEN
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(REPO, "a_dive_into_ray_tracing_amd", "bin", "rtmi_render")
+SEED = 1984
+
+
+@pytest.fixture(scope="module")
+def world():
+    return rt.random_scene()
+
+
+@pytest.fixture(scope="module")
+def renderer(world):
+    r = rt.Renderer(world, 0)
+    yield r
+    r.close()
+
+
+@pytest.mark.parametrize("passes", [[24], [1, 23], [7, 5, 12], [3] * 8])
+def test_passes_equal_single_render(passes, renderer):
+    W, H = 72, 48
+    cam = rt.final_camera(W / H)
+    want = renderer.render(cam, W, H, sum(passes), 50, SEED)
+    renderer.accum_reset(W, H)
+    s = 0
+    for k in passes:
+        renderer.render_pass(cam, W, H, s, k, 50, SEED)
+        s += k
+    assert np.array_equal(renderer.accum_resolve(), want)
+
+
+def test_passes_out_of_order_equal_single_render(renderer):
+    W, H = 40, 24
+    cam = rt.final_camera(W / H)
+    want = renderer.render(cam, W, H, 16, 50, SEED)
+    renderer.accum_reset(W, H)
+    for s0, k in [(10, 6), (0, 4), (4, 6)]:
+        renderer.render_pass(cam, W, H, s0, k, 50, SEED)
+    assert np.array_equal(renderer.accum_resolve(), want)
+
+
+def test_pass_on_row_strip_equals_render_rows(renderer):
+    import torch
+
+    W, H, S = 64, 40, 12
+    cam = rt.final_camera(W / H)
+    row0, step, nrows = 1, 3, 14  # rows 1, 4, ..., 40 (the last is past H: zero)
+    strip = torch.zeros((nrows, W, 3), dtype=torch.float32, device="cuda:0")
+    renderer.render_rows(cam, W, H, S, 50, SEED, row0, step, nrows, strip.data_ptr(), 0)
+    renderer.synchronize()
+    renderer.accum_reset(W, nrows)
+    renderer.render_pass(cam, W, H, 0, 5, 50, SEED, row0, step, nrows)
+    renderer.render_pass(cam, W, H, 5, 7, 50, SEED, row0, step, nrows)
+    assert np.array_equal(renderer.accum_resolve(), strip.cpu().numpy())
+
+
+def test_progressive_matches_oracle(world, renderer):
+    W, H, S = 48, 32, 9
+    cam = rt.final_camera(W / H)
+    got = renderer.progressive(cam, W, H, S, 4, 50, SEED)
+    oc = O.OrCamera()
+    import ctypes as C
+
+    C.memmove(C.byref(oc), C.byref(cam), C.sizeof(oc))
+    want = O.fast_render(O.Scene(world.center_radius, world.mat_kind, world.mat_params), oc, W, H, S, 50, SEED)
+    assert np.array_equal(got, want)
+
+
+def test_checkpoint_resume_in_fresh_context(world, renderer, tmp_path):
+    W, H, S = 64, 40, 20
+    cam = rt.final_camera(W / H)
+    ck = str(tmp_path / "run.ckpt")
+    want = renderer.render(cam, W, H, S, 50, SEED)
+    seen = []
+
+    class Stop(Exception):
+        pass
+
+    def stop_after_two(done):
+        seen.append(done)
+        if len(seen) == 2:
+            raise Stop
+
+    with pytest.raises(Stop):
+        renderer.progressive(cam, W, H, S, 6, 50, SEED, checkpoint=ck, on_pass=stop_after_two)
+    assert seen == [6, 12] and os.path.exists(ck)
+    fresh = rt.Renderer(world, 0)
+    try:
+        resumed = []
+        got = fresh.progressive(cam, W, H, S, 6, 50, SEED, checkpoint=ck, on_pass=resumed.append)
+        assert resumed == [18, 20]
+        assert np.array_equal(got, want)
+        with pytest.raises(rt.RTError, match="another render"):
+            fresh.progressive(cam, W, H, S, 6, 50, SEED + 1, checkpoint=ck)
+    finally:
+        fresh.close()
+
+
+def test_cli_checkpoint_resume_equals_single_render(tmp_path):
+    if not os.access(CLI, os.X_OK):
+        pytest.skip("CLI not built")
+    ck, a, b, pfm = (str(tmp_path / n) for n in ("c.ckpt", "a.ppm", "b.ppm", "b.pfm"))
+    base = [CLI, "--width", "96", "--seed", "7"]
+    r = subprocess.run(base + ["--spp", "10", "--pass-spp", "5", "--checkpoint", ck, "--out", "/dev/null"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run(base + ["--spp", "24", "--pass-spp", "5", "--checkpoint", ck, "--out", b, "--pfm", pfm],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert '"pass_done_spp": 15' in r.stderr and '"pass_done_spp": 5}' not in r.stderr  # resumed at 10
+    r = subprocess.run(base + ["--spp", "24", "--out", a], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert open(a, "rb").read() == open(b, "rb").read()
+    mean = rt.read_pfm(pfm)
+    assert mean.shape == (64, 96, 3) and np.isfinite(mean).all() and mean.min() >= 0
+
+
+# ------------------------------------------------------------ config 4 -----
+def _png_rgb(path):
+    from PIL import Image
+
+    return np.asarray(Image.open(path).convert("RGB"), dtype=np.float64)
+
+
+def test_config4_convergence(renderer):
+    W, H = 1200, 800
+    cam = rt.final_camera(W / H)
+    rms = {}
+    imgs = {}
+    for S in (50, 500, 5000):
+        a = renderer.progressive(cam, W, H, S, 500, 50, 1001)
+        b = renderer.progressive(cam, W, H, S, 500, 50, 2002)
+        d = a / S - b / S
+        rms[S] = float(np.sqrt((d * d).mean()))
+        imgs[S] = a
+    r1, r2 = rms[50] / rms[500], rms[500] / rms[5000]
+    print(f"seed-to-seed RMS {rms}; ratios {r1:.3f} {r2:.3f} (1/sqrt(S): {np.sqrt(10):.3f})")
+    assert abs(r1 / np.sqrt(10) - 1) < 0.12 and abs(r2 / np.sqrt(10) - 1) < 0.12
+    ref = _png_rgb(os.path.join(GOLD, "gallery_final.png"))
+    e500 = np.sqrt(((rt.quantize(imgs[500], 500) - ref) ** 2).mean())
+    e5000 = np.sqrt(((rt.quantize(imgs[5000], 5000) - ref) ** 2).mean())
+    print(f"RMSE vs gallery (500 spp reference): ours@500 {e500:.3f}, ours@5000 {e5000:.3f}")
+    # the reference's own noise at 500 spp is RMSE 1.795 / sqrt(2) = 1.27 levels
+    assert e5000 < e500 and e5000 < 1.5

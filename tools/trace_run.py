@@ -22,6 +22,7 @@ strip_of = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 chunk, tail, tchunk = (int(x) for x in (sys.argv[3:6] + ["0", "-1", "0"][len(sys.argv[3:6]):]))
 L = rt.load()
 L.rt_ctx_debug_trace.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32]
+L.rt_ctx_debug_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
 W, H, S = 1200, 800, 500
 r = rt.Renderer(rt.random_scene(), 0)
 r.set_kernel(kind)
@@ -34,6 +35,8 @@ buf = (C.c_uint64 * (4 * cap))()
 for it in range(2):
     r.render_rows(cam, W, H, S, 50, 1984, row0, step, nrows, strip.data_ptr(), 0)
     r.synchronize()
+    cnt = (C.c_uint64 * 8)()
+    L.rt_ctx_debug_counters(r._h, cnt)
     n = L.rt_ctx_debug_trace(r._h, buf, cap)
 t = np.frombuffer(buf, dtype=np.uint64, count=4 * n).reshape(n, 4).astype(np.float64)
 t0, t1 = t[:, 0], t[:, 1]
@@ -48,6 +51,7 @@ wid = (raw[:, 3] >> np.uint64(32)).astype(np.int64)
 hw = (raw[:, 2] >> np.uint64(32)).astype(np.int64)
 print(f"{kind} strip_of={strip_of} chunk={chunk} tail={tail}/{tchunk}: waves {n}, span {span / 1e3:.2f} ms, "
       f"items {items.sum()}, segs/wave-line mean {segs.mean():.0f}")
+print(f"cycles in hit_world_packed / wave lifetime: {cnt[5] / max(cnt[6], 1):.3f}")
 print("wave end percentiles (ms):", " ".join(f"p{q}={np.percentile(t1, q) / 1e3:.2f}" for q in (1, 10, 50, 90, 99, 100)))
 print("wave duration percentiles (ms):", " ".join(f"p{q}={np.percentile(t1 - t0, q) / 1e3:.3f}" for q in (1, 10, 50, 90, 99, 100)))
 bins = np.linspace(0, span, 21)

@@ -136,6 +136,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * kWavesPerBlock + wave;
+  if constexpr (BVH) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
   if (item >= a.n_items) return;  // wave-uniform; no block barrier follows
 
   int tile, s0, ns;
@@ -163,6 +164,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
   RTMI_TRACE_BEGIN
 #if RTMI_STATS
   unsigned stats[4] = {0, 0, 0, 0};  // groups, groups with a candidate (wave), resolves (lane), sphere resolves (wave)
+  unsigned bvh_stats[2] = {0, 0};    // BVH: node visits, leaf sphere tests (lane)
 #endif
 
   const SceneView<float> sc{geom, sh0, sh1, a.n};
@@ -203,7 +205,11 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
 #endif
       int k;
       if constexpr (BVH) {
-        k = hit_world_bvh<kPairGroup>(a.acc, o, d, t);
+        k = hit_world_bvh<kPairGroup>(a.acc, o, d, t
+#if RTMI_STATS
+                                      , bvh_stats
+#endif
+        );
       } else {
         k = hit_world_packed<kPairGroup>(pairs, a.npairs, o, d, t
 #if RTMI_STATS
@@ -266,6 +272,8 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
 #if RTMI_STATS
   if (lane == 0) { atomicAdd(&segments[1], (unsigned long long)stats[0]); atomicAdd(&segments[2], (unsigned long long)stats[1]); atomicAdd(&segments[4], (unsigned long long)stats[3]); }
   atomicAdd(&segments[3], (unsigned long long)stats[2]);
+  atomicAdd(&segments[5], (unsigned long long)bvh_stats[0]);
+  atomicAdd(&segments[6], (unsigned long long)bvh_stats[1]);
 #endif
   RTMI_TRACE_END(1)
   if (lane < nv) {
@@ -335,6 +343,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
   __shared__ unsigned long long wave_segs[kWavesPerBlock];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
+  if constexpr (BVH) stage_bvh(a.acc);
   for (int s = 0; s < 2; ++s)
     for (int c = 0; c < 3; ++c) acc[wave][s][c][lane] = 0;
   if (lane == 0) wave_segs[wave] = 0;
@@ -343,6 +352,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
   RTMI_TRACE_BEGIN
 #if RTMI_STATS
   unsigned stats[4] = {0, 0, 0, 0};
+  unsigned bvh_stats[2] = {0, 0};
 #endif
   const SceneView<float> sc{geom, sh0, sh1, a.n};
 
@@ -473,7 +483,11 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
 #endif
       int k;
       if constexpr (BVH) {
-        k = hit_world_bvh<kPairGroup>(a.acc, o, d, t);
+        k = hit_world_bvh<kPairGroup>(a.acc, o, d, t
+#if RTMI_STATS
+                                      , bvh_stats
+#endif
+        );
       } else {
         k = hit_world_packed<kPairGroup>(pairs, a.npairs, o, d, t
 #if RTMI_STATS
@@ -544,9 +558,34 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
 #if RTMI_STATS
   if (lane == 0) { atomicAdd(&segments[1], (unsigned long long)stats[0]); atomicAdd(&segments[2], (unsigned long long)stats[1]); atomicAdd(&segments[4], (unsigned long long)stats[3]); }
   atomicAdd(&segments[3], (unsigned long long)stats[2]);
+  atomicAdd(&segments[5], (unsigned long long)bvh_stats[0]);
+  atomicAdd(&segments[6], (unsigned long long)bvh_stats[1]);
 #endif
   RTMI_TRACE_END(n_taken)
   (void)n_taken;
+}
+
+// Closest hit of n given rays by the brute-force loop and by the BVH
+// (validation: rt_ctx_debug_hits).  rays = {o.xyz, d.xyz} per ray.
+__global__ __launch_bounds__(256) void debug_hit_kernel(const SpherePair *__restrict__ pairs, int32_t npairs, Accel acc,
+                                                       const float *__restrict__ rays, int32_t n,
+                                                       int32_t *__restrict__ out_idx, float *__restrict__ out_t) {
+  stage_bvh(acc);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const V3<float> o = mk(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
+  const V3<float> d = mk(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+  float t0, t1;
+#if RTMI_STATS
+  unsigned st[4] = {0, 0, 0, 0}, bst[2] = {0, 0};
+  out_idx[2 * i] = hit_world_packed<kPairGroup>(pairs, npairs, o, d, t0, st);
+  out_idx[2 * i + 1] = acc.nnodes ? hit_world_bvh<kPairGroup>(acc, o, d, t1, bst) : -2;
+#else
+  out_idx[2 * i] = hit_world_packed<kPairGroup>(pairs, npairs, o, d, t0);
+  out_idx[2 * i + 1] = acc.nnodes ? hit_world_bvh<kPairGroup>(acc, o, d, t1) : -2;
+#endif
+  out_t[2 * i] = t0;
+  out_t[2 * i + 1] = acc.nnodes ? t1 : 0.f;
 }
 
 __global__ void finalize_kernel(const unsigned long long *__restrict__ accum, float *__restrict__ out, size_t n) {
@@ -660,6 +699,8 @@ struct rt_ctx {
   int32_t nnodes = 0;
   float4 *bvh_sph = nullptr;
   int32_t *bvh_idx = nullptr;
+  int32_t nbvh_sph = 0;
+  int32_t resident_blocks_bvh = 0;  // persistent grid with the BVH's LDS
   hipStream_t last_stream = nullptr;
   int32_t tile_w = 8;
   int32_t chunk = 0;       // phase-1 samples per item (0 = automatic)
@@ -771,6 +812,8 @@ RTMI_EXPORT int rt_ctx_destroy(rt_ctx *ctx) {
 }
 
 namespace {
+constexpr size_t kBvhLdsMax = 64 * 1024;  // BVH bytes staged per block
+
 // BVH over the small spheres: median split on the longest centroid axis,
 // leaves of <= kLeafMax spheres, nodes in DFS order with skip links.  Boxes
 // are the spheres' double-precision bounds grown by a margin (1e-3 of the
@@ -807,7 +850,7 @@ struct BvhBuilder {
       nd.bmax[a] = std::nextafter(float(hi[a]), INFINITY);
     }
     if (cnt <= kLeafMax) {
-      nd.leaf = (int32_t(sph.size()) << 3) | cnt;
+      nd.leaf = (int32_t(sph.size()) << 4) | cnt;
       for (int i = 0; i < cnt; ++i) {
         sph.push_back(g[ids[i]]);
         idx.push_back(ids[i]);
@@ -947,7 +990,18 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
     }
     ctx->nbig = int32_t(big.size());
     ctx->nbig_pairs = nb_pad / 2;
-    ctx->nnodes = int32_t(b.nodes.size());
+    ctx->nbvh_sph = int32_t(b.sph.size());
+    // the BVH must fit in LDS beside the accumulators; otherwise it is not
+    // offered (RT_ACCEL_BVH renders brute force)
+    const size_t lds = bvh_lds_bytes(int32_t(b.nodes.size()), int32_t(b.sph.size()));
+    ctx->nnodes = lds <= kBvhLdsMax ? int32_t(b.nodes.size()) : 0;
+    int per_cu = 0;
+    if (ctx->nnodes)
+      HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<8, true, true>,
+                                                           64 * kWavesPerBlock, lds));
+    int cus = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    ctx->resident_blocks_bvh = std::max(1, per_cu) * cus;
   }
   ctx->n = n;
   return RT_OK;
@@ -985,22 +1039,24 @@ namespace {
 template <int TW, bool BVH>
 void launch_persistent(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a,
                        unsigned long long *accum, float *out) {
+  const size_t lds = BVH ? bvh_lds_bytes(a.acc.nnodes, a.acc.nsph) : 0;
   if (chunked)
-    hipLaunchKernelGGL((render_persistent<TW, true, BVH>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
+    hipLaunchKernelGGL((render_persistent<TW, true, BVH>), grid, dim3(64 * kWavesPerBlock), lds, st, ctx->geom, ctx->sh0,
                        ctx->sh1, ctx->pairs, a, accum, out, ctx->segments, ctx->counter);
   else
-    hipLaunchKernelGGL((render_persistent<TW, false, BVH>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom,
+    hipLaunchKernelGGL((render_persistent<TW, false, BVH>), grid, dim3(64 * kWavesPerBlock), lds, st, ctx->geom,
                        ctx->sh0, ctx->sh1, ctx->pairs, a, accum, out, ctx->segments, ctx->counter);
 }
 
 template <int TW, bool BVH>
 void launch_tw(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a,
                unsigned long long *accum, float *out) {
+  const size_t lds = BVH ? bvh_lds_bytes(a.acc.nnodes, a.acc.nsph) : 0;
   if (chunked)
-    hipLaunchKernelGGL((render_kernel<TW, true, BVH>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
+    hipLaunchKernelGGL((render_kernel<TW, true, BVH>), grid, dim3(64 * kWavesPerBlock), lds, st, ctx->geom, ctx->sh0,
                        ctx->sh1, ctx->pairs, a, accum, out, ctx->segments);
   else
-    hipLaunchKernelGGL((render_kernel<TW, false, BVH>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
+    hipLaunchKernelGGL((render_kernel<TW, false, BVH>), grid, dim3(64 * kWavesPerBlock), lds, st, ctx->geom, ctx->sh0,
                        ctx->sh1, ctx->pairs, a, accum, out, ctx->segments);
 }
 
@@ -1052,8 +1108,9 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   // 1/4 33.4 vs 36.5, 1/8 17.9 vs 19.3); one wave per item on a whole frame
   // (128.2 vs 130.4 ms).  Both give the same image.
   const int64_t tile_samples = tiles * int64_t(spp);
+  const bool bvh = ctx->accel == RT_ACCEL_BVH && ctx->nnodes > 0;
   const bool persistent = ctx->kernel == RT_KERNEL_PERSISTENT ||
-                          (ctx->kernel == RT_KERNEL_AUTO && tile_samples < 6000000);
+                          (ctx->kernel == RT_KERNEL_AUTO && !bvh && tile_samples < 6000000);
   int32_t chunk1 = ctx->chunk, chunk2 = ctx->tail_chunk, tail = ctx->tail_spp;
   if (chunk1 <= 0 && persistent) {
     // ~28 items per resident wave (1/8 strip: chunk 8 -> 17.5 ms, 16 -> 17.9, 32 -> 19.7)
@@ -1103,17 +1160,18 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   if (int64_t(tiles_y) * TH < nvalid || int64_t(tiles_x) * TW < W || nch1 * int64_t(chunk1) < spp1 ||
       nch2 * int64_t(chunk2) < spp - spp1)
     return set_error(RT_EHIP, "internal: work items do not cover the image");
-  const bool bvh = ctx->accel == RT_ACCEL_BVH && ctx->nnodes > 0;
   if (bvh) {
-    a.acc = Accel{ctx->big_pairs, ctx->big_idx, ctx->nbig_pairs, ctx->nnodes, ctx->nodes, ctx->bvh_sph, ctx->bvh_idx};
+    a.acc = Accel{ctx->big_pairs, ctx->big_idx, ctx->nbig_pairs, ctx->nnodes, ctx->nodes, ctx->bvh_sph, ctx->bvh_idx,
+                  ctx->nbvh_sph};
   } else {
-    a.acc = Accel{nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr};
+    a.acc = Accel{nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr, 0};
   }
   dim3 grid;
   if (persistent) {
     // a resident grid of waves pulling items from a global counter
     HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
-    const int64_t waves = std::min<int64_t>(items, int64_t(ctx->resident_blocks) * kWavesPerBlock);
+    const int64_t waves =
+        std::min<int64_t>(items, int64_t(bvh ? ctx->resident_blocks_bvh : ctx->resident_blocks) * kWavesPerBlock);
     grid = dim3(unsigned((waves + kWavesPerBlock - 1) / kWavesPerBlock));
   } else {
     grid = dim3(unsigned((items + kWavesPerBlock - 1) / kWavesPerBlock));
@@ -1431,6 +1489,36 @@ RTMI_EXPORT int rt_ctx_debug_trace(rt_ctx *ctx, uint64_t *out, int32_t cap) {
   (void)cap;
   return 0;
 #endif
+}
+
+// Validation: brute-force and BVH closest hits of n rays (host arrays):
+// rays[6n] = o.xyz d.xyz; idx[2n] = {brute, bvh} sphere index (-1 miss);
+// t[2n] likewise.  Not part of the render path.
+RTMI_EXPORT int rt_ctx_debug_hits(rt_ctx *ctx, const float *rays, int32_t n, int32_t *idx, float *t) {
+  if (!ctx || !rays || !idx || !t || n < 0) return set_error(RT_EINVAL, "rt_ctx_debug_hits: bad argument");
+  if (n == 0) return RT_OK;
+  if (ctx->n <= 0) return set_error(RT_EINVAL, "no scene");
+  DeviceGuard guard(ctx->device);
+  float *d_rays = nullptr, *d_t = nullptr;
+  int32_t *d_idx = nullptr;
+  int rc;
+  if ((rc = dev_alloc(&d_rays, size_t(n) * 6)) || (rc = dev_alloc(&d_idx, size_t(n) * 2)) ||
+      (rc = dev_alloc(&d_t, size_t(n) * 2)))
+    return rc;
+  HIP_TRY(hipMemcpy(d_rays, rays, size_t(n) * 6 * sizeof(float), hipMemcpyHostToDevice));
+  const Accel acc{ctx->big_pairs, ctx->big_idx, ctx->nbig_pairs, ctx->nnodes, ctx->nodes, ctx->bvh_sph, ctx->bvh_idx,
+                  ctx->nbvh_sph};
+  const size_t lds = ctx->nnodes ? bvh_lds_bytes(ctx->nnodes, ctx->nbvh_sph) : 0;
+  hipLaunchKernelGGL(debug_hit_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), lds, ctx->stream, ctx->pairs,
+                     ctx->npairs, acc, d_rays, n, d_idx, d_t);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  HIP_TRY(hipMemcpy(idx, d_idx, size_t(n) * 2 * sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(t, d_t, size_t(n) * 2 * sizeof(float), hipMemcpyDeviceToHost));
+  (void)hipFree(d_rays);
+  (void)hipFree(d_idx);
+  (void)hipFree(d_t);
+  return RT_OK;
 }
 
 RTMI_EXPORT int rt_ctx_debug_counters(rt_ctx *ctx, uint64_t *out) {

@@ -530,9 +530,16 @@ struct BvhNode {
   float bmin[3];
   int32_t skip;  // next node when this subtree is not entered (DFS order; leaf: index + 1)
   float bmax[3];
-  int32_t leaf;  // -1: inner node (first child = index + 1); else first << 3 | count (1..kLeafMax)
+  int32_t leaf;  // -1: inner node (first child = index + 1); else first << 4 | count (1..kLeafMax)
 };
-constexpr int kLeafMax = 4;
+#ifndef RTMI_BVH_LEAF
+#define RTMI_BVH_LEAF 4
+#endif
+#ifndef RTMI_BOX_FMA
+#define RTMI_BOX_FMA 1
+#endif
+constexpr int kLeafMax = RTMI_BVH_LEAF;
+static_assert(kLeafMax >= 1 && kLeafMax <= 15, "leaf size");
 
 struct Accel {
   const SpherePair *big;     // packed pairs of the big spheres (padded like the scene)
@@ -542,10 +549,33 @@ struct Accel {
   const BvhNode *nodes;
   const float4 *sph;         // BVH spheres in leaf order: {cx, cy, cz, S}
   const int32_t *sph_idx;    // their scene indices
+  int32_t nsph;
 };
 
+// The BVH lives in LDS during a launch (dynamic shared memory, staged by
+// every block at its start): the traversal is a chain of dependent node
+// loads, ~100 cycles from LDS against ~500+ from L2.  Layout: nodes as
+// 2*nnodes float4, then nsph sphere float4s, then nsph int32 indices.
+extern __shared__ float4 rtmi_bvh_lds[];
+__host__ __device__ constexpr size_t bvh_lds_bytes(int32_t nnodes, int32_t nsph) {
+  return size_t(2 * nnodes + nsph) * 16 + size_t(nsph) * 4;
+}
+
+__device__ __forceinline__ void stage_bvh(const Accel &g) {
+  const float4 *nodes = reinterpret_cast<const float4 *>(g.nodes);
+  for (int i = threadIdx.x; i < 2 * g.nnodes; i += blockDim.x) rtmi_bvh_lds[i] = nodes[i];
+  for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) rtmi_bvh_lds[2 * g.nnodes + i] = g.sph[i];
+  int32_t *idx = reinterpret_cast<int32_t *>(rtmi_bvh_lds + 2 * g.nnodes + g.nsph);
+  for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) idx[i] = g.sph_idx[i];
+  __syncthreads();
+}
+
 template <int GP>
-__device__ __forceinline__ int32_t hit_world_bvh(const Accel &acc_s, V3<float> o, V3<float> d, float &t_hit) {
+__device__ __forceinline__ int32_t hit_world_bvh(const Accel &acc_s, V3<float> o, V3<float> d, float &t_hit
+#if RTMI_STATS
+                                                 , unsigned *bstats
+#endif
+                                                 ) {
   const float a = dot<true>(d, d);
   const float inv_a = 1.0f / a;
   const float K = dot<true>(o, d);
@@ -601,15 +631,35 @@ __device__ __forceinline__ int32_t hit_world_bvh(const Accel &acc_s, V3<float> o
       }
     }
   }
-  // 2. the BVH, stackless: per-lane walk of the DFS node array with skip links
-  const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+  // 2. the BVH (staged in LDS by stage_bvh), stackless: per-lane walk of the
+  // DFS node array with skip links
+  const float4 *lds_sph = rtmi_bvh_lds + 2 * acc_s.nnodes;
+  const int32_t *lds_idx = reinterpret_cast<const int32_t *>(rtmi_bvh_lds + 2 * acc_s.nnodes + acc_s.nsph);
+  // inverse direction with |d_i| clamped to >= 1e-20: no infinities, so no
+  // 0*inf or inf-inf NaNs in the slab test (min/max would not ignore them
+  // reliably).  The clamp moves the ray by a negligible angle; a ray running
+  // parallel to a slab plane within ~1e-6 of it cannot reach a sphere, which
+  // sits at least the box margin inside every face.
+  auto safe_inv = [](float v) { return 1.0f / (__builtin_fabsf(v) < 1e-20f ? __builtin_copysignf(1e-20f, v) : v); };
+  const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
+#if RTMI_BOX_FMA
+  // slab distances as one fma per plane: (b - o) * i = fma(b, i, -o*i); the
+  // box margin covers the different rounding
+  const float ox = -o.x * ix, oy = -o.y * iy, oz = -o.z * iz;
+#endif
   int32_t node = 0;
   while (node < acc_s.nnodes) {
-    const float4 lo = *reinterpret_cast<const float4 *>(&acc_s.nodes[node].bmin[0]);
-    const float4 hi = *reinterpret_cast<const float4 *>(&acc_s.nodes[node].bmax[0]);
+    const float4 lo = rtmi_bvh_lds[2 * node];
+    const float4 hi = rtmi_bvh_lds[2 * node + 1];
+#if RTMI_BOX_FMA
+    const float tx0 = __builtin_fmaf(lo.x, ix, ox), tx1 = __builtin_fmaf(hi.x, ix, ox);
+    const float ty0 = __builtin_fmaf(lo.y, iy, oy), ty1 = __builtin_fmaf(hi.y, iy, oy);
+    const float tz0 = __builtin_fmaf(lo.z, iz, oz), tz1 = __builtin_fmaf(hi.z, iz, oz);
+#else
     const float tx0 = (lo.x - o.x) * ix, tx1 = (hi.x - o.x) * ix;
     const float ty0 = (lo.y - o.y) * iy, ty1 = (hi.y - o.y) * iy;
     const float tz0 = (lo.z - o.z) * iz, tz1 = (hi.z - o.z) * iz;
+#endif
     const float tnear = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx0, tx1), __builtin_fminf(ty0, ty1)),
                                         __builtin_fminf(tz0, tz1));
     const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx0, tx1), __builtin_fmaxf(ty0, ty1)),
@@ -618,14 +668,20 @@ __device__ __forceinline__ int32_t hit_world_bvh(const Accel &acc_s, V3<float> o
     // keeps ties at the interval ends on the safe side
     const bool enter = tnear <= tfar * 1.0001f + 1e-6f && tfar >= 0.0f && tnear <= t_max * 1.0001f + 1e-6f;
     const int32_t leaf = __float_as_int(hi.w);
+#if RTMI_STATS
+    bstats[0] += 1;
+#endif
     if (enter && leaf >= 0) {
-      const int32_t first = leaf >> 3, cnt = leaf & 7;
+      const int32_t first = leaf >> 4, cnt = leaf & 15;
+#if RTMI_STATS
+      bstats[1] += cnt;
+#endif
       for (int32_t k = first; k < first + cnt; ++k) {
-        const float4 s = acc_s.sph[k];
+        const float4 s = lds_sph[k];
         const float hb = __builtin_fmaf(-s.x, d.x, __builtin_fmaf(-s.y, d.y, __builtin_fmaf(-s.z, d.z, K)));
         const float acc = __builtin_fmaf(mx, s.x, __builtin_fmaf(my, s.y, __builtin_fmaf(mz, s.z, __builtin_fmaf(a, s.w, aL))));
         const float disc = __builtin_fmaf(hb, hb, -acc);
-        if (!(disc < 0.0f)) resolve(acc_s.sph_idx[k], hb, disc);
+        if (!(disc < 0.0f)) resolve(lds_idx[k], hb, disc);
       }
     }
     node = enter ? node + 1 : __float_as_int(lo.w);

@@ -346,3 +346,37 @@ def test_bvh_config2_equals_brute_force(config2, final_renderer):
     finally:
         final_renderer.set_accel("none")
     assert np.array_equal(got, img)
+
+
+def test_bvh_adversarial_rays_equal_brute_force(final_world):
+    """1M random rays: origins in the field and just off sphere surfaces
+    (both sides), directions with exactly-zero components; the BVH's closest
+    hit (index and t) equals the brute-force loop's for every ray
+    (rt_ctx_debug_hits, a validation entry point)."""
+    r = rt.Renderer(final_world, 0)
+    L = rt.load()
+    L.rt_ctx_debug_hits.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_float)]
+    n = 1_000_000
+    g = np.random.default_rng(11)
+    o = np.column_stack([g.uniform(-13, 13, n), g.uniform(-0.1, 3, n), g.uniform(-13, 13, n)])
+    k = g.integers(0, len(final_world), n // 2)
+    c, rad = final_world.center_radius[k, :3], np.abs(final_world.center_radius[k, 3])
+    u = g.normal(size=(n // 2, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    o[: n // 2] = c + u * (rad[:, None] * (1 + g.choice([1e-3, 1e-4, -1e-4, 1e-6, 0.0], n // 2)[:, None]))
+    dv = g.normal(size=(n, 3)) * g.choice([0.3, 1.0, 3.0], n)[:, None]
+    dv[g.random((n, 3)) < 0.03] = 0.0
+    dv[np.all(dv == 0, axis=1)] = [0, -1, 0]
+    rays = np.ascontiguousarray(np.column_stack([o, dv]).astype(np.float32))
+    idx = np.zeros(2 * n, np.int32)
+    t = np.zeros(2 * n, np.float32)
+    try:
+        rc = L.rt_ctx_debug_hits(r._h, rays.ctypes.data_as(C.POINTER(C.c_float)), n, idx.ctypes.data_as(C.POINTER(C.c_int32)),
+                                 t.ctypes.data_as(C.POINTER(C.c_float)))
+    finally:
+        r.close()
+    assert rc == 0
+    idx, t = idx.reshape(n, 2), t.reshape(n, 2)
+    assert (idx[:, 0] >= 0).mean() > 0.5
+    assert np.array_equal(idx[:, 0], idx[:, 1])
+    assert np.array_equal(t[:, 0], t[:, 1])

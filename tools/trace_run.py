@@ -26,6 +26,7 @@ L.rt_ctx_debug_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
 W, H, S = 1200, 800, 500
 r = rt.Renderer(rt.random_scene(), 0)
 r.set_kernel(kind)
+r.set_accel(os.environ.get("TRACE_ACCEL", "none"))
 r.set_schedule(chunk, tail, tchunk)
 cam = rt.final_camera(1.5)
 row0, step, nrows = rdist.strip_rows(H, 0, strip_of)

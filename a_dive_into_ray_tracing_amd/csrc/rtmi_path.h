@@ -562,8 +562,9 @@ __host__ __device__ constexpr size_t bvh_lds_bytes(int32_t nnodes, int32_t nsph)
 }
 
 __device__ __forceinline__ void stage_bvh(const Accel &g) {
+  // nodes split into a lo[] and a hi[] array (independent LDS loads)
   const float4 *nodes = reinterpret_cast<const float4 *>(g.nodes);
-  for (int i = threadIdx.x; i < 2 * g.nnodes; i += blockDim.x) rtmi_bvh_lds[i] = nodes[i];
+  for (int i = threadIdx.x; i < 2 * g.nnodes; i += blockDim.x) rtmi_bvh_lds[(i & 1) * g.nnodes + (i >> 1)] = nodes[i];
   for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) rtmi_bvh_lds[2 * g.nnodes + i] = g.sph[i];
   int32_t *idx = reinterpret_cast<int32_t *>(rtmi_bvh_lds + 2 * g.nnodes + g.nsph);
   for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) idx[i] = g.sph_idx[i];
@@ -647,10 +648,11 @@ __device__ __forceinline__ int32_t hit_world_bvh(const Accel &acc_s, V3<float> o
   // box margin covers the different rounding
   const float ox = -o.x * ix, oy = -o.y * iy, oz = -o.z * iz;
 #endif
+  const float4 *lds_lo = rtmi_bvh_lds, *lds_hi = rtmi_bvh_lds + acc_s.nnodes;
   int32_t node = 0;
   while (node < acc_s.nnodes) {
-    const float4 lo = rtmi_bvh_lds[2 * node];
-    const float4 hi = rtmi_bvh_lds[2 * node + 1];
+    const float4 lo = lds_lo[node];
+    const float4 hi = lds_hi[node];
 #if RTMI_BOX_FMA
     const float tx0 = __builtin_fmaf(lo.x, ix, ox), tx1 = __builtin_fmaf(hi.x, ix, ox);
     const float ty0 = __builtin_fmaf(lo.y, iy, oy), ty1 = __builtin_fmaf(hi.y, iy, oy);
@@ -660,13 +662,16 @@ __device__ __forceinline__ int32_t hit_world_bvh(const Accel &acc_s, V3<float> o
     const float ty0 = (lo.y - o.y) * iy, ty1 = (hi.y - o.y) * iy;
     const float tz0 = (lo.z - o.z) * iz, tz1 = (hi.z - o.z) * iz;
 #endif
+    // slab interval clipped to [0, t_max].  No slack is needed: a sphere
+    // that can be hit lies >= the box margin inside the box, so its chord
+    // starts after tnear and ends before tfar by far more than rounding, and
+    // a hit at t_hit >= 0.001 with t_hit <= t_max (ties included) keeps the
+    // box entered.
     const float tnear = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx0, tx1), __builtin_fminf(ty0, ty1)),
-                                        __builtin_fminf(tz0, tz1));
+                                        __builtin_fmaxf(__builtin_fminf(tz0, tz1), 0.0f));
     const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx0, tx1), __builtin_fmaxf(ty0, ty1)),
-                                       __builtin_fmaxf(tz0, tz1));
-    // slack on both ends: the box margin already covers float error; this
-    // keeps ties at the interval ends on the safe side
-    const bool enter = tnear <= tfar * 1.0001f + 1e-6f && tfar >= 0.0f && tnear <= t_max * 1.0001f + 1e-6f;
+                                       __builtin_fminf(__builtin_fmaxf(tz0, tz1), t_max));
+    const bool enter = tnear <= tfar;
     const int32_t leaf = __float_as_int(hi.w);
 #if RTMI_STATS
     bstats[0] += 1;

@@ -12,10 +12,18 @@ gathered to rank 0 with ONE RCCL gather (torch.distributed "nccl" = RCCL)
 inside the timed region.  Total work is fixed as N grows: scaling "strong".
 value = W*H*spp*K / max-over-ranks(wall time of K steps) / 1e6.
 
-roofline: FP32 VALU bound.  achieved = segments * 18 * 487 FLOP per launch
+Closest hits go through the BVH by default (--accel bvh): the same closest
+hit as the brute-force loop, bit for bit (tests/test_gpu_parity.py), so the
+same image.  --accel none times the brute-force kernel.
+
+roofline: FP32 VALU.  achieved = segments * 18 * 487 FLOP per launch
 (SURVEY §8(d): 18 flops per ray-sphere test, brute force over 487 spheres;
 segments = world.hit calls, counted exactly on the GPU) / mean launch time
 from HIP events on the launch stream; peak = 157.3 TFLOP/s FP32 vector.
+With the BVH this is the brute-force-equivalent ("work_equivalent", as
+SURVEY §8(d) prescribes for culling), so frac can exceed 1; roofline.
+brute_force gives the brute-force kernel's own figure from one extra,
+untimed launch of the same rows.
 cpu_baseline: the reference itself (oracle/_ref/ref_harness: worker() at -O2,
 16 std::threads as the reference's concurrency) on a bounded sample, rank 0,
 N = 1 only.
@@ -83,7 +91,8 @@ def main():
     ap.add_argument("--tail-spp", type=int, default=-1)
     ap.add_argument("--tail-chunk", type=int, default=0)
     ap.add_argument("--kernel", choices=["auto", "persistent", "grid"], default="auto")
-    ap.add_argument("--accel", choices=["none", "bvh"], default="none")
+    ap.add_argument("--accel", choices=["none", "bvh"], default="bvh",
+                    help="closest-hit search: bvh (default; same image bit for bit) or brute force")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--strip-of", type=int, default=0,
                     help="analysis only: time ONE rank's interleaved strip of an N-GPU run on this GPU")
@@ -167,6 +176,23 @@ def main():
     else:
         total_segs, kernel_ms_max = float(segs), kernel_ms
 
+    # The brute-force kernel's own VALU roofline, beside the BVH's
+    # work-equivalent one: one more launch of the same rows, untimed.
+    bf = None
+    if args.accel != "none":
+        r.set_accel("none")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        r.render_rows(cam, W, H, SPP, DEPTH, SEED, row0, row_step, nrows, strip.data_ptr(), stream.cuda_stream)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        bf_ms = e0.elapsed_time(e1)
+        bf_segs = r.last_segments()
+        r.set_accel(args.accel)
+        bf_ach = bf_segs * FLOP_PER_SPHERE_TEST * len(world) / (bf_ms * 1e-3) / 1e12
+        bf = {"kernel_ms": round(bf_ms, 3), "achieved": round(bf_ach, 3), "frac": round(bf_ach / PEAK_FP32_TFLOPS, 4),
+              "note": "brute-force kernel (RT_ACCEL_NONE) on the same rows: the FP32 VALU roofline proper"}
+
     if rank == 0 and N > 1:  # the gathered image is whole: every row rendered, none twice
         img = rdist.unpermute([g.cpu().numpy() for g in gathered], H)
         assert np.isfinite(img).all() and (img.reshape(H, -1).max(axis=1) > 0).all(), "incomplete gathered image"
@@ -218,6 +244,7 @@ def main():
                 # with the BVH the FLOP count stays the brute-force figure
                 # ("work-equivalent"), so frac can pass 1
                 "work_equivalent": args.accel != "none",
+                "brute_force": bf,
             },
             "vs_baseline_ref": "published CPU rt_in_one_weekend 0.1189 Msamples/s (README.md:16-19)",
         }

@@ -205,7 +205,7 @@ def main():
         pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             try:
-                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+                traffic = (json.load(open(pmc)).get(args.accel) or {}).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         line = {

@@ -1,18 +1,24 @@
-"""Summarise rocprofv3 PMC csvs of the render kernel: per-dispatch sums."""
+"""Summarise rocprofv3 PMC csvs of the render kernels: per-dispatch means,
+grouped by kernel (BVH vs brute force).  usage: pmc_summary.py DIR"""
 import collections
 import csv
 import glob
 import sys
 
 root = sys.argv[1]
-vals = collections.defaultdict(list)
+vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(f"{root}/pmc*/*_counter_collection.csv")):
     per = collections.defaultdict(float)
+    names = {}
     for r in csv.DictReader(open(f)):
-        if "render_kernel" in r["Kernel_Name"] or "render_persistent" in r["Kernel_Name"]:
+        k = r["Kernel_Name"]
+        if "render_kernel" in k or "render_persistent" in k:
             per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
-    for (d, c), v in per.items():
-        vals[c].append(v)
-for c in sorted(vals):
-    v = vals[c]
-    print(f"{c:32s} mean {sum(v)/len(v):.4g}  (n={len(v)})")
+            names[r["Dispatch_Id"]] = k.split("(")[0]
+    for (dsp, c), v in per.items():
+        vals[names[dsp]][c].append(v)
+for k in sorted(vals):
+    print(k)
+    for c in sorted(vals[k]):
+        v = vals[k][c]
+        print(f"  {c:32s} mean {sum(v)/len(v):.4g}  (n={len(v)})")

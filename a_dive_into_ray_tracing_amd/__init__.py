@@ -182,6 +182,11 @@ class Renderer:
     def set_kernel(self, kind="auto"):
         check(self.L.rt_ctx_set_kernel(self._h, self.KERNELS[kind]), "rt_ctx_set_kernel")
 
+    ORDERINGS = {"none": 0, "cost": 1}  # RT_ORDER_* (include/rtmi.h)
+
+    def set_ordering(self, ordering="cost"):
+        check(self.L.rt_ctx_set_ordering(self._h, self.ORDERINGS[ordering]), "rt_ctx_set_ordering")
+
     ACCELS = {"none": 0, "bvh": 1}  # RT_ACCEL_* (include/rtmi.h)
 
     def set_accel(self, accel="none"):

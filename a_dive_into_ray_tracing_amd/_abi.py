@@ -65,6 +65,7 @@ SIGNATURES = {
     "rt_ctx_set_schedule": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
     "rt_ctx_set_kernel": (C.c_int, [C.c_void_p, C.c_int32]),
     "rt_ctx_set_accel": (C.c_int, [C.c_void_p, C.c_int32]),
+    "rt_ctx_set_ordering": (C.c_int, [C.c_void_p, C.c_int32]),
     "rt_ctx_accel_info": (C.c_int, [C.c_void_p, _ip, _ip]),
     "rt_render": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_uint64, _fp]),
     "rt_render_rows": (

@@ -28,6 +28,7 @@
 // default).  The DOUBLE instantiation (FAST=false) reproduces the reference
 // bit-for-bit given its rand() stream (rt_replay_worker).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -62,6 +63,10 @@ struct RenderArgs {
   int32_t s_base;
   uint64_t out_elems;  // elements of accum / out (RTMI_CHECK builds verify every write)
   Accel acc;           // BVH kernels only
+  // cost-ordered dispatch: tile rank -> tile (null: identity)
+  // and per-tile world.hit counts of this launch (null: not measured)
+  const int32_t *tile_order;
+  unsigned *tile_cost;
 };
 
 #ifndef RTMI_WAVES_PER_BLOCK
@@ -150,6 +155,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
     s0 = a.spp1 + (i2 - tile * a.nch2) * a.chunk2;
     ns = min(a.chunk2, a.spp - s0);
   }
+  if (a.tile_order) tile = a.tile_order[tile];  // expensive tiles first
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
   const int x0 = tx * TW, y0 = ty * TH;
   const int vw = min(TW, a.W - x0), vh = min(TH, a.nrows_valid - y0);
@@ -268,7 +274,10 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
   atomicAdd(&wave_segs[wave], (unsigned long long)nseg);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  if (lane == 0) atomicAdd(segments, wave_segs[wave]);
+  if (lane == 0) {
+    atomicAdd(segments, wave_segs[wave]);
+    if (a.tile_cost) atomicAdd(&a.tile_cost[tile], unsigned(wave_segs[wave]));
+  }
 #if RTMI_STATS
   if (lane == 0) { atomicAdd(&segments[1], (unsigned long long)stats[0]); atomicAdd(&segments[2], (unsigned long long)stats[1]); atomicAdd(&segments[4], (unsigned long long)stats[3]); }
   atomicAdd(&segments[3], (unsigned long long)stats[2]);
@@ -305,7 +314,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
 // So no lane waits for the slowest path of an item, and the grid's tail is a
 // few paths long.  Same per-path arithmetic as render_kernel (bit-identical).
 struct ItemDesc {
-  int x0, y0, vw, nv, s0, nq;
+  int x0, y0, vw, nv, s0, nq, tile;
 };
 
 template <int TW>
@@ -322,6 +331,7 @@ __device__ __forceinline__ ItemDesc describe_item(const RenderArgs &a, int item)
     s0 = a.spp1 + (i2 - tile * a.nch2) * a.chunk2;
     ns = min(a.chunk2, a.spp - s0);
   }
+  if (a.tile_order) tile = a.tile_order[tile];  // expensive tiles first
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
   ItemDesc r;
   r.x0 = tx * TW;
@@ -331,6 +341,7 @@ __device__ __forceinline__ ItemDesc describe_item(const RenderArgs &a, int item)
   r.nv = r.vw * vh;
   r.s0 = s0;
   r.nq = r.nv * ns;
+  r.tile = tile;
   return r;
 }
 
@@ -341,9 +352,11 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
     float *__restrict__ out, unsigned long long *__restrict__ segments, unsigned *__restrict__ counter) {
   __shared__ unsigned long long acc[kWavesPerBlock][2][3][64];
   __shared__ unsigned long long wave_segs[kWavesPerBlock];
+  __shared__ unsigned slot_segs[kWavesPerBlock][2];  // world.hit calls of each slot's item (tile cost)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if constexpr (BVH) stage_bvh(a.acc);
+  if (lane < 2) slot_segs[wave][lane] = 0;
   for (int s = 0; s < 2; ++s)
     for (int c = 0; c < 3; ++c) acc[wave][s][c][lane] = 0;
   if (lane == 0) wave_segs[wave] = 0;
@@ -373,11 +386,11 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
   int cur = 0;
   bool cur_valid = false, prev_valid = false, exhausted = false;
   int cur_next = 0;
-  ItemDesc cd{0, 0, 1, 0, 0, 0}, pd{0, 0, 1, 0, 0, 0};
+  ItemDesc cd{0, 0, 1, 0, 0, 0, 0}, pd{0, 0, 1, 0, 0, 0, 0};
 
   // per-lane path state
   V3<float> o, d, T;
-  int px = 0, depth = 0, lane_slot = 0;
+  int px = 0, depth = 0, lane_slot = 0, path_segs = 0;
   bool active = false;
   Xoro rng;
 
@@ -399,6 +412,10 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
       }
     }
     for (int c = 0; c < 3; ++c) acc[wave][s][c][lane] = 0;
+    if (lane == 0) {
+      if (a.tile_cost) atomicAdd(&a.tile_cost[it.tile], slot_segs[wave][s]);
+      slot_segs[wave][s] = 0;
+    }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   };
 
@@ -478,6 +495,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
     if (active) {
       float t;
       ++nseg;
+      ++path_segs;
 #if RTMI_TRACE
       const unsigned long long cyc0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -533,6 +551,8 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
     }
 #endif
     if (done) {
+      atomicAdd(&slot_segs[wave][lane_slot], unsigned(path_segs));
+      path_segs = 0;
       atomicAdd(&acc[wave][lane_slot][0][px], (unsigned long long)to_fixed(col.x));
       atomicAdd(&acc[wave][lane_slot][1][px], (unsigned long long)to_fixed(col.y));
       atomicAdd(&acc[wave][lane_slot][2][px], (unsigned long long)to_fixed(col.z));
@@ -701,7 +721,18 @@ struct rt_ctx {
   int32_t *bvh_idx = nullptr;
   int32_t nbvh_sph = 0;
   int32_t resident_blocks_bvh = 0;  // persistent grid with the BVH's LDS
+  // cost-ordered dispatch: per-tile world.hit counts of the
+  // last render with the same tile layout order the next one's tiles
+  int32_t ordering = RT_ORDER_COST;
+  unsigned *cost_prev = nullptr, *cost_cur = nullptr, *cost_sorted = nullptr;
+  int32_t *order = nullptr, *iota = nullptr;
+  size_t cost_cap = 0;  // tiles
+  void *sort_tmp = nullptr;
+  size_t sort_tmp_bytes = 0;
+  bool cost_valid = false;
+  int64_t cost_key[6] = {0, 0, 0, 0, 0, 0};  // W, H, row0, row_step, nvalid, tile_w
   hipStream_t last_stream = nullptr;
+  hipEvent_t last_done = nullptr;  // end of the last render's work on last_stream
   int32_t tile_w = 8;
   int32_t chunk = 0;       // phase-1 samples per item (0 = automatic)
   int32_t tail_spp = -1;   // samples in the short-item phase (-1 = automatic)
@@ -783,6 +814,7 @@ RTMI_EXPORT int rt_ctx_create(int32_t device, rt_ctx **out) {
   auto ctx = std::make_unique<rt_ctx>();
   ctx->device = device;
   HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&ctx->last_done, hipEventDisableTiming));
   if (int rc = dev_alloc(&ctx->segments, 8)) return rc;
   HIP_TRY(hipMemset(ctx->segments, 0, 8 * sizeof(unsigned long long)));
   if (int rc = dev_alloc(&ctx->counter, 1)) return rc;
@@ -804,9 +836,12 @@ RTMI_EXPORT int rt_ctx_destroy(rt_ctx *ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   for (void *p : {(void *)ctx->geom, (void *)ctx->sh0, (void *)ctx->sh1, (void *)ctx->geom64, (void *)ctx->sh064,
                   (void *)ctx->sh164, (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments, (void *)ctx->pairs, (void *)ctx->counter, (void *)ctx->pass_accum,
-                  (void *)ctx->big_pairs, (void *)ctx->big_idx, (void *)ctx->nodes, (void *)ctx->bvh_sph, (void *)ctx->bvh_idx})
+                  (void *)ctx->big_pairs, (void *)ctx->big_idx, (void *)ctx->nodes, (void *)ctx->bvh_sph, (void *)ctx->bvh_idx,
+                  (void *)ctx->cost_prev, (void *)ctx->cost_cur, (void *)ctx->cost_sorted, (void *)ctx->order,
+                  (void *)ctx->iota, ctx->sort_tmp})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(ctx->stream);
+  if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
   delete ctx;
   return RT_OK;
 }
@@ -880,6 +915,14 @@ struct BvhBuilder {
   }
 };
 }  // namespace
+
+RTMI_EXPORT int rt_ctx_set_ordering(rt_ctx *ctx, int32_t ordering) {
+  if (!ctx) return set_error(RT_EINVAL, "null ctx");
+  if (ordering != RT_ORDER_NONE && ordering != RT_ORDER_COST) return set_error(RT_EINVAL, "unknown ordering %d", ordering);
+  ctx->ordering = ordering;
+  ctx->cost_valid = false;
+  return RT_OK;
+}
 
 RTMI_EXPORT int rt_ctx_set_accel(rt_ctx *ctx, int32_t accel) {
   if (!ctx) return set_error(RT_EINVAL, "null ctx");
@@ -1079,7 +1122,15 @@ void launch_shape(bool persistent, bool bvh, bool chunked, dim3 grid, hipStream_
 int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t spp, int32_t max_depth,
                      uint64_t seed, int32_t row0, int32_t row_step, int32_t nrows, float *strip, hipStream_t st,
                      int32_t s_base = 0, unsigned long long *pass_accum = nullptr) {
+  // The context's buffers (accumulator, counters, cost maps) are reused by
+  // every render: a render on another stream first waits for the last one.
+  if (ctx->last_stream && ctx->last_stream != st) HIP_TRY(hipStreamWaitEvent(st, ctx->last_done, 0));
   ctx->last_stream = st;
+  struct MarkDone {  // record the end of this render's work, whatever path returns
+    rt_ctx *c;
+    hipStream_t s;
+    ~MarkDone() { (void)hipEventRecord(c->last_done, s); }
+  } mark_done{ctx, st};
   HIP_TRY(hipMemsetAsync(ctx->segments, 0, 8 * sizeof(unsigned long long), st));
   if (nrows == 0) return RT_OK;
   // valid rows: row0 + r*row_step < H
@@ -1166,6 +1217,48 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   } else {
     a.acc = Accel{nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr, 0};
   }
+  // cost-ordered dispatch: tiles sorted by the previous render's per-tile
+  // world.hit counts (same layout), most expensive first, so the dispatch
+  // tail is made of cheap items.  Changes the order of work only.
+  a.tile_order = nullptr;
+  a.tile_cost = nullptr;
+  if (ctx->ordering == RT_ORDER_COST) {
+    const int64_t key[6] = {W, H, row0, row_step, nvalid, TW};
+    if (ctx->cost_cap < size_t(tiles)) {
+      int rc;
+      if ((rc = dev_alloc(&ctx->cost_prev, size_t(tiles))) || (rc = dev_alloc(&ctx->cost_cur, size_t(tiles))) ||
+          (rc = dev_alloc(&ctx->cost_sorted, size_t(tiles))) || (rc = dev_alloc(&ctx->order, size_t(tiles))) ||
+          (rc = dev_alloc(&ctx->iota, size_t(tiles)))) {
+        ctx->cost_cap = 0;
+        return rc;
+      }
+      std::vector<int32_t> io(static_cast<size_t>(tiles));
+      for (int64_t t = 0; t < tiles; ++t) io[size_t(t)] = int32_t(t);
+      HIP_TRY(hipMemcpy(ctx->iota, io.data(), io.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+      ctx->cost_cap = size_t(tiles);
+      ctx->cost_valid = false;
+      size_t need = 0;
+      HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, need, ctx->cost_prev, ctx->cost_sorted, ctx->iota,
+                                                           ctx->order, int(tiles)));
+      if (need > ctx->sort_tmp_bytes) {
+        if (ctx->sort_tmp) (void)hipFree(ctx->sort_tmp);
+        ctx->sort_tmp = nullptr;
+        HIP_TRY(hipMalloc(&ctx->sort_tmp, need));
+        ctx->sort_tmp_bytes = need;
+      }
+    }
+    if (ctx->cost_valid && std::equal(key, key + 6, ctx->cost_key)) {
+      size_t bytes = ctx->sort_tmp_bytes;
+      HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(ctx->sort_tmp, bytes, ctx->cost_prev, ctx->cost_sorted,
+                                                           ctx->iota, ctx->order, int(tiles), 0, 32, st));
+      a.tile_order = ctx->order;
+    }
+    HIP_TRY(hipMemsetAsync(ctx->cost_cur, 0, size_t(tiles) * sizeof(unsigned), st));
+    a.tile_cost = ctx->cost_cur;
+    std::swap(ctx->cost_prev, ctx->cost_cur);  // this launch's counts order the next one
+    std::copy(key, key + 6, ctx->cost_key);
+    ctx->cost_valid = true;
+  }
   dim3 grid;
   if (persistent) {
     // a resident grid of waves pulling items from a global counter
@@ -1224,6 +1317,7 @@ RTMI_EXPORT int rt_accum_reset(rt_ctx *ctx, int32_t W, int32_t nrows) {
   ctx->pass_W = W;
   ctx->pass_rows = nrows;
   ctx->pass_spp = 0;
+  if (ctx->last_stream) HIP_TRY(hipStreamSynchronize(ctx->last_stream));  // no pass still adding
   if (n) HIP_TRY(hipMemsetAsync(ctx->pass_accum, 0, n * sizeof(unsigned long long), ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return RT_OK;
@@ -1254,6 +1348,7 @@ RTMI_EXPORT int rt_accum_resolve(rt_ctx *ctx, float *dev_sum, float *host_sum, v
   if (!dev_sum && !host_sum) return set_error(RT_EINVAL, "rt_accum_resolve: no output");
   DeviceGuard guard(ctx->device);
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  if (ctx->last_stream && ctx->last_stream != st) HIP_TRY(hipStreamWaitEvent(st, ctx->last_done, 0));
   const size_t n = size_t(ctx->pass_W) * size_t(ctx->pass_rows) * 3;
   float *out = dev_sum;
   if (!out) {
@@ -1295,6 +1390,7 @@ RTMI_EXPORT int rt_accum_import(rt_ctx *ctx, const int64_t *host, size_t n, int3
     return set_error(RT_EINVAL, "rt_accum_import: size %zu, accumulator %zu (call rt_accum_reset)", n, want);
   if (spp_done < 0) return set_error(RT_EINVAL, "rt_accum_import: negative sample count");
   DeviceGuard guard(ctx->device);
+  if (ctx->last_stream) HIP_TRY(hipStreamSynchronize(ctx->last_stream));
   HIP_TRY(hipMemcpy(ctx->pass_accum, host, n * sizeof(int64_t), hipMemcpyHostToDevice));
   ctx->pass_spp = spp_done;
   return RT_OK;

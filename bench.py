@@ -93,6 +93,7 @@ def main():
     ap.add_argument("--kernel", choices=["auto", "persistent", "grid"], default="auto")
     ap.add_argument("--accel", choices=["none", "bvh"], default="bvh",
                     help="closest-hit search: bvh (default; same image bit for bit) or brute force")
+    ap.add_argument("--ordering", choices=["cost", "none"], default="cost")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--strip-of", type=int, default=0,
                     help="analysis only: time ONE rank's interleaved strip of an N-GPU run on this GPU")
@@ -121,6 +122,7 @@ def main():
     r.set_schedule(args.chunk, args.tail_spp, args.tail_chunk)
     r.set_kernel(args.kernel)
     r.set_accel(args.accel)
+    r.set_ordering(args.ordering)
     row0, row_step, nrows = rdist.strip_rows(H, rank, N)  # interleaved rows, row j -> rank j % N
     if args.strip_of > 1 and N == 1:  # analysis mode: one rank's share of an N-GPU render
         row0, row_step, nrows = rdist.strip_rows(H, 0, args.strip_of)
@@ -228,6 +230,7 @@ def main():
                 "tile": f"{args.tile_w}x{64 // args.tile_w}",
                 "kernel": args.kernel,
                 "accel": args.accel,
+                "ordering": args.ordering,
             },
             "roofline": {
                 "bound": "valu",

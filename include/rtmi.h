@@ -146,6 +146,14 @@ int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind);
  * the same closest hit, bit for bit.  rt_ctx_accel_info
  * reports the split (big spheres, BVH nodes) of the current scene. */
 enum { RT_ACCEL_NONE = 0, RT_ACCEL_BVH = 1 };
+
+/* Dispatch order.  RT_ORDER_COST (default): every render counts world.hit
+ * calls per tile, and the next render with the same tile layout dispatches
+ * its tiles most-expensive-first (a GPU radix sort of those counts), so the
+ * end of the launch is cheap work.  RT_ORDER_NONE: tiles in image order.
+ * Never changes the image. */
+enum { RT_ORDER_NONE = 0, RT_ORDER_COST = 1 };
+int rt_ctx_set_ordering(rt_ctx *ctx, int32_t ordering);
 int rt_ctx_set_accel(rt_ctx *ctx, int32_t accel);
 int rt_ctx_accel_info(rt_ctx *ctx, int32_t *n_big, int32_t *n_nodes);
 

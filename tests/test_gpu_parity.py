@@ -380,3 +380,28 @@ def test_bvh_adversarial_rays_equal_brute_force(final_world):
     assert (idx[:, 0] >= 0).mean() > 0.5
     assert np.array_equal(idx[:, 0], idx[:, 1])
     assert np.array_equal(t[:, 0], t[:, 1])
+
+
+@pytest.mark.parametrize("kernel,accel", [("grid", "none"), ("persistent", "none"), ("grid", "bvh"), ("persistent", "bvh")])
+def test_cost_ordered_dispatch_same_image(kernel, accel, final_world, final_renderer):
+    """RT_ORDER_COST: the second render of a layout dispatches tiles by the
+    first one's per-tile cost; the image is the same bit for bit (and equals
+    the oracle's)."""
+    W, H, S = 120, 72, 12
+    cam = rt.final_camera(W / H)
+    final_renderer.set_kernel(kernel)
+    final_renderer.set_accel(accel)
+    try:
+        final_renderer.set_ordering("none")
+        plain = final_renderer.render(cam, W, H, S, 50, SEED)
+        final_renderer.set_ordering("cost")
+        first = final_renderer.render(cam, W, H, S, 50, SEED)
+        ordered = final_renderer.render(cam, W, H, 2 * S, 50, SEED + 1)  # same layout: ordered by `first`
+        again = final_renderer.render(cam, W, H, S, 50, SEED)
+    finally:
+        final_renderer.set_kernel("auto")
+        final_renderer.set_accel("none")
+        final_renderer.set_ordering("cost")
+    assert np.array_equal(first, plain) and np.array_equal(again, plain)
+    want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, 2 * S, 50, SEED + 1)
+    assert np.array_equal(ordered, want)

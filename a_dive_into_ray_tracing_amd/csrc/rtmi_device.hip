@@ -188,8 +188,10 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render
     const int i = x0 + lx;
     const int j = a.row0 + (y0 + ly) * a.row_step;
     rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(a.s_base + s));
-    const float u = (float(i) + rng.uni()) / float(a.W - 1);  // main.cpp:278
-    const float v = (float(j) + rng.uni()) / float(a.H - 1);  // main.cpp:279
+    float ju, jv;
+    rng.pair(ju, jv);
+    const float u = (float(i) + ju) / float(a.W - 1);  // main.cpp:278
+    const float v = (float(j) + jv) / float(a.H - 1);  // main.cpp:279
     get_ray<true, float>(a.cam, u, v, rng, o, d);
     T = mk(1.f, 1.f, 1.f);
     depth = 0;
@@ -435,8 +437,10 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
           const int i = cd.x0 + lx;
           const int j = a.row0 + (cd.y0 + ly) * a.row_step;
           rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(a.s_base + cd.s0 + qs));
-          const float u = (float(i) + rng.uni()) / float(a.W - 1);  // main.cpp:278
-          const float v = (float(j) + rng.uni()) / float(a.H - 1);  // main.cpp:279
+          float ju, jv;
+          rng.pair(ju, jv);
+          const float u = (float(i) + ju) / float(a.W - 1);  // main.cpp:278
+          const float v = (float(j) + jv) / float(a.H - 1);  // main.cpp:279
           get_ray<true, float>(a.cam, u, v, rng, o, d);
           T = mk(1.f, 1.f, 1.f);
           depth = 0;

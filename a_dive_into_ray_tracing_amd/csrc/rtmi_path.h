@@ -9,6 +9,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "../../include/rtmi.h"
 
@@ -111,7 +112,60 @@ struct Xoro {
   }
   // top 24 bits: uniform on [0,1) exactly representable in float
   __device__ __forceinline__ float uni() { return float(uint32_t(next() >> 40)) * 0x1p-24f; }
+  // two uniforms from one step: bits 63..40 and 39..16
+  __device__ __forceinline__ void pair(float &u, float &v) {
+    const uint64_t r = next();
+    u = float(uint32_t(r >> 40)) * 0x1p-24f;
+    v = float(uint32_t(r >> 16) & 0xFFFFFFu) * 0x1p-24f;
+  }
 };
+
+// cos and sin of 2*pi*v, v in [0,1) a multiple of 2^-24: exact quadrant
+// reduction, then Cephes' sinf/cosf polynomials on [-pi/4, pi/4] with
+// explicit fma — the oracle's sincos2pi, operation for operation.
+__device__ __forceinline__ void sincos2pi(float v, float &c, float &s) {
+  const float t = v * 4.0f;
+  const int k = int(t + 0.5f);
+  const float x = (t - float(k)) * 1.57079637f;
+  const float x2 = x * x;
+  float p = __builtin_fmaf(x2, -1.9515295891e-4f, 8.3321608736e-3f);
+  p = __builtin_fmaf(x2, p, -1.6666654611e-1f);
+  const float sn = __builtin_fmaf(x * x2, p, x);
+  float q = __builtin_fmaf(x2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+  q = __builtin_fmaf(x2, q, 4.166664568298827e-2f);
+  const float cs = __builtin_fmaf(x2 * x2, q, __builtin_fmaf(-0.5f, x2, 1.0f));
+  const int m = k & 3;
+  c = m == 0 ? cs : m == 1 ? -sn : m == 2 ? -cs : sn;
+  s = m == 0 ? sn : m == 1 ? cs : m == 2 ? -sn : -cs;
+}
+// Fast-mode sampling without rejection loops (a wavefront would run a
+// rejection loop until its unluckiest lane succeeds): the same
+// distributions as unit_vector(random_in_unit_sphere()),
+// random_in_unit_sphere() and random_in_unit_disk() (vec3.h:103-130);
+// DESIGN.md §3.2.
+__device__ __forceinline__ V3<float> unit_dir(Xoro &g) {
+  float u, v, c, s;
+  g.pair(u, v);
+  const float z = __builtin_fmaf(-2.0f, u, 1.0f);
+  const float r = __builtin_sqrtf(__builtin_fmaf(-z, z, 1.0f));
+  sincos2pi(v, c, s);
+  return mk(r * c, r * s, z);
+}
+__device__ __forceinline__ V3<float> in_sphere_direct(Xoro &g) {
+  const V3<float> d = unit_dir(g);
+  float a, b, c, unused;
+  g.pair(a, b);
+  g.pair(c, unused);
+  const float r = __builtin_fmaxf(a, __builtin_fmaxf(b, c));
+  return mk(r * d.x, r * d.y, r * d.z);
+}
+__device__ __forceinline__ V3<float> in_disk_direct(Xoro &g) {
+  float u, v, c, s;
+  g.pair(u, v);
+  const float r = __builtin_sqrtf(u);
+  sincos2pi(v, c, s);
+  return mk(r * c, r * s, 0.0f);
+}
 
 // Replays a supplied glibc rand() stream: random_double() = rand()/(RAND_MAX+1.0)
 struct StreamRng {
@@ -173,7 +227,9 @@ template <class R> struct Cam {
 // camera::get_ray camera.h:56-62
 template <bool F, class R, class G>
 __device__ __forceinline__ void get_ray(const Cam<R> &c, R s, R t, G &g, V3<R> &o, V3<R> &d) {
-  const V3<R> p = in_disk<F, R>(g);
+  V3<R> p;
+  if constexpr (std::is_same<G, Xoro>::value) p = in_disk_direct(g);
+  else p = in_disk<F, R>(g);
   const R rdx = c.lens * p.x, rdy = c.lens * p.y;
   const V3<R> off = mk(madd<F>(rdy, c.v.x, rdx * c.u.x), madd<F>(rdy, c.v.y, rdx * c.u.y),
                        madd<F>(rdy, c.v.z, rdx * c.u.z));
@@ -703,7 +759,9 @@ __device__ __forceinline__ bool scatter(const SceneView<R> &sc, int32_t k, V3<R>
   const auto s1 = sc.sh1[k];
   const int kind = int(s1.x);
   if (kind == RT_MAT_LAMBERTIAN) {  // material.h:19-31
-    const V3<R> ru = unit<F>(in_sphere<F, R>(g));
+    V3<R> ru;
+    if constexpr (std::is_same<G, Xoro>::value) ru = unit_dir(g);
+    else ru = unit<F>(in_sphere<F, R>(g));
     V3<R> dir = mk(normal.x + ru.x, normal.y + ru.y, normal.z + ru.z);
     if (near_zero(dir)) dir = normal;
     dout = dir;
@@ -712,7 +770,9 @@ __device__ __forceinline__ bool scatter(const SceneView<R> &sc, int32_t k, V3<R>
   }
   if (kind == RT_MAT_METAL) {  // material.h:40-49
     const V3<R> refl = reflect<F>(unit<F>(din), normal);
-    const V3<R> rv = in_sphere<F, R>(g);
+    V3<R> rv;
+    if constexpr (std::is_same<G, Xoro>::value) rv = in_sphere_direct(g);
+    else rv = in_sphere<F, R>(g);
     const R fz = s1.y;
     const V3<R> dir = mk(madd<F>(fz, rv.x, refl.x), madd<F>(fz, rv.y, refl.y), madd<F>(fz, rv.z, refl.z));
     dout = dir;

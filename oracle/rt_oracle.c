@@ -83,6 +83,33 @@ static inline uint64_t xo_next(xo *g) {
 }
 /* top 24 bits -> [0,1) exactly representable in float */
 static inline float xo_uni(xo *g) { return (float)(uint32_t)(xo_next(g) >> 40) * 0x1p-24f; }
+/* two uniforms from one step: bits 63..40 and 39..16 */
+static inline void xo_pair(xo *g, float *u, float *v) {
+  uint64_t r = xo_next(g);
+  *u = (float)(uint32_t)(r >> 40) * 0x1p-24f;
+  *v = (float)(uint32_t)((r >> 16) & 0xFFFFFFu) * 0x1p-24f;
+}
+/* cos and sin of 2*pi*v, v in [0,1) a multiple of 2^-24: exact quadrant
+ * reduction, then Cephes' sinf/cosf polynomials on [-pi/4, pi/4] with
+ * explicit fmaf (the GPU evaluates the identical sequence). */
+static inline void sincos2pi(float v, float *c, float *s) {
+  const float t = v * 4.0f;
+  const int k = (int)(t + 0.5f);
+  const float x = (t - (float)k) * 1.57079637f;
+  const float x2 = x * x;
+  float p = fmaf(x2, -1.9515295891e-4f, 8.3321608736e-3f);
+  p = fmaf(x2, p, -1.6666654611e-1f);
+  const float sn = fmaf(x * x2, p, x);
+  float q = fmaf(x2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+  q = fmaf(x2, q, 4.166664568298827e-2f);
+  const float cs = fmaf(x2 * x2, q, fmaf(-0.5f, x2, 1.0f));
+  switch (k & 3) {
+    case 0: *c = cs; *s = sn; break;
+    case 1: *c = -sn; *s = cs; break;
+    case 2: *c = -cs; *s = -sn; break;
+    default: *c = sn; *s = -cs; break;
+  }
+}
 
 void or_fast_rng(uint64_t seed, uint64_t pixel, uint32_t sample, int32_t n, uint64_t *out) {
   xo g;
@@ -95,6 +122,7 @@ void or_fast_rng(uint64_t seed, uint64_t pixel, uint32_t sample, int32_t n, uint
 /* ---------------------------------------------------------------------- */
 #define RAY_OFFSET 0
 #define HIT_EXPANDED 0
+#define DIRECT_SAMPLING 0
 #define PFX(x) ref_##x
 #define R double
 #define MADD(a, b, c) ((a) * (b) + (c))
@@ -120,6 +148,7 @@ void or_fast_rng(uint64_t seed, uint64_t pixel, uint32_t sample, int32_t n, uint
 #undef T_STACK
 #undef RAY_OFFSET
 #undef HIT_EXPANDED
+#undef DIRECT_SAMPLING
 
 /* ---------------------------------------------------------------------- */
 /* fast instantiation: float, fmaf policy, xoroshiro, forward product.      */
@@ -131,6 +160,7 @@ static inline float pow5f(float x) {
 }
 #define RAY_OFFSET 1
 #define HIT_EXPANDED 1
+#define DIRECT_SAMPLING 1
 #define PFX(x) fast_##x
 #define R float
 #define MADD(a, b, c) fmaf((a), (b), (c))
@@ -154,6 +184,29 @@ static inline float pow5f(float x) {
 #undef UNI
 #undef ROOT
 #undef T_STACK
+
+/* Test hook: n draws of the fast-mode direct samplers (kind 0: unit
+ * direction, 1: point in the unit ball, 2: point in the unit disk) from the
+ * stream (seed, pixel 0, sample 0), as xyz triples; 3: (cos, sin, v) of
+ * 2 pi v for v = (i * 4099 mod 2^24) * 2^-24 (sincos2pi accuracy). */
+void or_fast_dirs(int32_t kind, uint64_t seed, int32_t n, float *out) {
+  xo g;
+  xo_init(&g, seed, 0, 0);
+  for (int32_t i = 0; i < n; i++) {
+    fast_V p = {0, 0, 0};
+    if (kind == 0) p = fast_unit_dir(&g);
+    else if (kind == 1) p = fast_in_sphere_direct(&g);
+    else if (kind == 2) p = fast_in_disk_direct(&g);
+    else {
+      float c, s, v = (float)(((int64_t)i * 4099) & 0xFFFFFF) * 0x1p-24f;
+      sincos2pi(v, &c, &s);
+      p.x = c; p.y = s; p.z = v;
+    }
+    out[3 * i] = p.x;
+    out[3 * i + 1] = p.y;
+    out[3 * i + 2] = p.z;
+  }
+}
 
 /* ---------------------------------------------------------------------- */
 /* Scenes and camera (host, double)                                         */

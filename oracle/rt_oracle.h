@@ -96,6 +96,9 @@ int32_t or_fast_sample(const or_scene *s, const or_camera *c, int32_t W, int32_t
                        float out[3]);
 /* xoroshiro128+ stream for key (seed, pixel, sample): first n raw outputs. */
 void or_fast_rng(uint64_t seed, uint64_t pixel, uint32_t sample, int32_t n, uint64_t *out);
+/* n draws of the fast-mode direct samplers (kind 0 unit direction, 1 unit
+ * ball, 2 unit disk; 3 sincos2pi on a v grid) as xyz triples. */
+void or_fast_dirs(int32_t kind, uint64_t seed, int32_t n, float *out);
 /* Total path segments (world.hit calls) of the fast-mode render, for the
  * algorithmic-work accounting of bench.py. */
 int64_t or_fast_segments(const or_scene *s, const or_camera *c, int32_t W, int32_t H,

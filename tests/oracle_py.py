@@ -74,6 +74,7 @@ def lib():
         L.or_fast_sample.argtypes = [C.POINTER(OrScene), C.POINTER(OrCamera)] + [C.c_int32] * 3 + [C.c_uint64] + [C.c_int32] * 3 + [_fp]
         L.or_fast_sample.restype = C.c_int32
         L.or_fast_rng.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_int32, C.POINTER(C.c_uint64)]
+        L.or_fast_dirs.argtypes = [C.c_int32, C.c_uint64, C.c_int32, C.POINTER(C.c_float)]
         _lib = L
     return _lib
 

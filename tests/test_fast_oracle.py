@@ -68,3 +68,48 @@ def test_fast_rng_streams_distinct():
     assert not np.array_equal(a, b)
     O.lib().or_fast_rng(1984, 6, 0, 8, b.ctypes.data_as(C.POINTER(C.c_uint64)))
     assert not np.array_equal(a, b)
+
+
+def _dirs(kind, n=400_000, seed=7):
+    out = np.zeros(3 * n, np.float32)
+    O.lib().or_fast_dirs(kind, seed, n, out.ctypes.data_as(C.POINTER(C.c_float)))
+    return out.reshape(n, 3).astype(np.float64)
+
+
+def test_sincos2pi_accuracy():
+    p = _dirs(3, n=1 << 16)
+    ang = 2 * np.pi * p[:, 2]
+    assert np.abs(p[:, 0] - np.cos(ang)).max() < 4e-7
+    assert np.abs(p[:, 1] - np.sin(ang)).max() < 4e-7
+
+
+def test_direct_unit_direction_is_uniform_on_sphere():
+    """unit_vector(random_in_unit_sphere()) in distribution: unit length,
+    zero mean, isotropic second moments, uniform z and azimuth."""
+    p = _dirs(0)
+    n = len(p)
+    assert np.abs(np.linalg.norm(p, axis=1) - 1).max() < 1e-6
+    assert np.abs(p.mean(axis=0)).max() < 5 / np.sqrt(n)
+    m2 = (p * p).mean(axis=0)
+    assert np.abs(m2 - 1 / 3).max() < 5 * 0.3 / np.sqrt(n)
+    hist, _ = np.histogram(np.arctan2(p[:, 1], p[:, 0]), bins=16)
+    assert np.abs(hist / (n / 16) - 1).max() < 0.03
+
+
+def test_direct_point_in_ball_radius_cdf():
+    """random_in_unit_sphere() in distribution: P(|p| < r) = r^3, isotropic."""
+    p = _dirs(1)
+    r = np.linalg.norm(p, axis=1)
+    assert r.max() < 1.0
+    for q in (0.25, 0.5, 0.75, 0.9):
+        assert abs((r < q).mean() - q ** 3) < 0.004
+    assert np.abs(p.mean(axis=0)).max() < 0.005
+
+
+def test_direct_point_in_disk():
+    """random_in_unit_disk() in distribution: P(|p| < r) = r^2, z = 0."""
+    p = _dirs(2)
+    r = np.hypot(p[:, 0], p[:, 1])
+    assert r.max() < 1.0 and not p[:, 2].any()
+    for q in (0.25, 0.5, 0.75, 0.9):
+        assert abs((r < q).mean() - q ** 2) < 0.004

@@ -99,7 +99,7 @@ __device__ unsigned g_trace_n;
       g_trace[4 * k_ + 1] = __builtin_amdgcn_s_memrealtime();                            \
       g_trace[4 * k_ + 2] = (uint64_t(__builtin_amdgcn_s_getreg(0xF804)) << 32) |        \
                             uint64_t(unsigned(items));                                   \
-      g_trace[4 * k_ + 3] = (uint64_t(blockIdx.x * kWavesPerBlock + wave) << 32) |        \
+      g_trace[4 * k_ + 3] = (uint64_t(blockIdx.x * (blockDim.x >> 6) + wave) << 32) |     \
                             (wave_segs[wave] & 0xFFFFFFFFull);                           \
     }                                                                                    \
   }
@@ -130,17 +130,27 @@ constexpr int kPairGroup = RTMI_PAIR_GROUP;  // sphere pairs per scalar-load gro
 __device__ __forceinline__ int64_t to_fixed(float c) { return int64_t(c * 4294967296.0f); }
 __device__ __forceinline__ float from_fixed(int64_t v) { return float(v) * 0x1p-32f; }
 
+// Grid-kernel block shape.  The BVH kernel is latency-bound on its chain of
+// LDS node loads: 8-wave blocks (one staged BVH per 8 waves) at 8 waves per
+// SIMD (64 VGPRs, a few spilled) run config 2 in 52.9 ms against 54.4 with
+// 4-wave blocks at 6 waves per SIMD (LDS-limited); the brute-force loop does
+// not gain (115.4 vs 114.4 ms) and keeps 4-wave blocks.
+template <bool BVH> struct GridShape {
+  static constexpr int waves = BVH ? 8 : kWavesPerBlock;
+  static constexpr int per_eu = BVH ? 8 : RTMI_WAVES_PER_EU;
+};
 template <int TW, bool CHUNKED, bool BVH>
-__global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_WAVES_PER_EU) void render_kernel(
+__global__ __launch_bounds__(64 * GridShape<BVH>::waves, GridShape<BVH>::per_eu) void render_kernel(
     const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1,
     const SpherePair *__restrict__ pairs, RenderArgs a, unsigned long long *__restrict__ accum,
     float *__restrict__ out, unsigned long long *__restrict__ segments) {
   constexpr int TH = 64 / TW;
-  __shared__ unsigned long long acc[kWavesPerBlock][3][64];
-  __shared__ unsigned long long wave_segs[kWavesPerBlock];
+  constexpr int WPB = GridShape<BVH>::waves;
+  __shared__ unsigned long long acc[WPB][3][64];
+  __shared__ unsigned long long wave_segs[WPB];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int item = blockIdx.x * kWavesPerBlock + wave;
+  const int item = blockIdx.x * WPB + wave;
   if constexpr (BVH) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
   if (item >= a.n_items) return;  // wave-uniform; no block barrier follows
 
@@ -1100,10 +1110,10 @@ void launch_tw(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const
                unsigned long long *accum, float *out) {
   const size_t lds = BVH ? bvh_lds_bytes(a.acc.nnodes, a.acc.nsph) : 0;
   if (chunked)
-    hipLaunchKernelGGL((render_kernel<TW, true, BVH>), grid, dim3(64 * kWavesPerBlock), lds, st, ctx->geom, ctx->sh0,
+    hipLaunchKernelGGL((render_kernel<TW, true, BVH>), grid, dim3(64 * GridShape<BVH>::waves), lds, st, ctx->geom, ctx->sh0,
                        ctx->sh1, ctx->pairs, a, accum, out, ctx->segments);
   else
-    hipLaunchKernelGGL((render_kernel<TW, false, BVH>), grid, dim3(64 * kWavesPerBlock), lds, st, ctx->geom, ctx->sh0,
+    hipLaunchKernelGGL((render_kernel<TW, false, BVH>), grid, dim3(64 * GridShape<BVH>::waves), lds, st, ctx->geom, ctx->sh0,
                        ctx->sh1, ctx->pairs, a, accum, out, ctx->segments);
 }
 
@@ -1184,7 +1194,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   chunk2 = std::min(chunk2, std::max(tail, 1));
   const int32_t nch2 = tail > 0 ? (tail + chunk2 - 1) / chunk2 : 0;
   const int64_t items = tiles * (int64_t(nch1) + nch2);
-  if (items > int64_t(INT32_MAX) - kWavesPerBlock) return set_error(RT_EINVAL, "too many work items");
+  if (items > int64_t(INT32_MAX) - 8) return set_error(RT_EINVAL, "too many work items");
   RenderArgs a;
   a.cam = cam_f(cam);
   a.n = ctx->n;
@@ -1271,7 +1281,8 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
         std::min<int64_t>(items, int64_t(bvh ? ctx->resident_blocks_bvh : ctx->resident_blocks) * kWavesPerBlock);
     grid = dim3(unsigned((waves + kWavesPerBlock - 1) / kWavesPerBlock));
   } else {
-    grid = dim3(unsigned((items + kWavesPerBlock - 1) / kWavesPerBlock));
+    const int64_t wpb = bvh ? GridShape<true>::waves : GridShape<false>::waves;
+    grid = dim3(unsigned((items + wpb - 1) / wpb));
   }
   switch (TW) {
     case 8: launch_shape<8>(persistent, bvh, chunked, grid, st, ctx, a, accum, strip); break;

@@ -223,7 +223,7 @@ __global__ __launch_bounds__(64 * GridShape<BVH>::waves, GridShape<BVH>::per_eu)
 #endif
       int k;
       if constexpr (BVH) {
-        k = hit_world_bvh<kPairGroup>(a.acc, o, d, t
+        k = hit_world_bvh<kBigGroup>(a.acc, o, d, t
 #if RTMI_STATS
                                       , bvh_stats
 #endif
@@ -515,7 +515,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
 #endif
       int k;
       if constexpr (BVH) {
-        k = hit_world_bvh<kPairGroup>(a.acc, o, d, t
+        k = hit_world_bvh<kBigGroup>(a.acc, o, d, t
 #if RTMI_STATS
                                       , bvh_stats
 #endif
@@ -613,10 +613,10 @@ __global__ __launch_bounds__(256) void debug_hit_kernel(const SpherePair *__rest
 #if RTMI_STATS
   unsigned st[4] = {0, 0, 0, 0}, bst[2] = {0, 0};
   out_idx[2 * i] = hit_world_packed<kPairGroup>(pairs, npairs, o, d, t0, st);
-  out_idx[2 * i + 1] = acc.nnodes ? hit_world_bvh<kPairGroup>(acc, o, d, t1, bst) : -2;
+  out_idx[2 * i + 1] = acc.nnodes ? hit_world_bvh<kBigGroup>(acc, o, d, t1, bst) : -2;
 #else
   out_idx[2 * i] = hit_world_packed<kPairGroup>(pairs, npairs, o, d, t0);
-  out_idx[2 * i + 1] = acc.nnodes ? hit_world_bvh<kPairGroup>(acc, o, d, t1) : -2;
+  out_idx[2 * i + 1] = acc.nnodes ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : -2;
 #endif
   out_t[2 * i] = t0;
   out_t[2 * i + 1] = acc.nnodes ? t1 : 0.f;
@@ -1015,13 +1015,13 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
     std::vector<int32_t> big, small;
     double scale = 0;
     for (int k = 0; k < n; k++) {
-      (rad[k] > 4 * med ? big : small).push_back(k);
-      if (rad[k] <= 4 * med)
+      (rad[k] > RTMI_BIG_FACTOR * med ? big : small).push_back(k);
+      if (rad[k] <= RTMI_BIG_FACTOR * med)
         for (int a = 0; a < 3; ++a) scale = std::max(scale, std::fabs(scene->center_radius[4 * k + a]) + rad[k]);
     }
     BvhBuilder b{scene->center_radius, g, 1e-3 * (1.0 + scale), {}, {}, {}};
     if (!small.empty()) b.build(small.data(), int(small.size()));
-    const int nb_pad = big.empty() ? 0 : (int(big.size()) + 2 * kPairGroup - 1) / (2 * kPairGroup) * (2 * kPairGroup);
+    const int nb_pad = big.empty() ? 0 : (int(big.size()) + 2 * kBigGroup - 1) / (2 * kBigGroup) * (2 * kBigGroup);
     std::vector<SpherePair> bp(nb_pad / 2 + kPairGroup);
     std::vector<int32_t> bidx(size_t(nb_pad) + 2 * kPairGroup, -1);
     for (auto &p : bp) {

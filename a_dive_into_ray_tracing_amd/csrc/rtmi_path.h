@@ -595,6 +595,13 @@ struct BvhNode {
 #define RTMI_BOX_FMA 1
 #endif
 constexpr int kLeafMax = RTMI_BVH_LEAF;
+#ifndef RTMI_BIG_FACTOR
+#define RTMI_BIG_FACTOR 4
+#endif
+#ifndef RTMI_BIG_GROUP
+#define RTMI_BIG_GROUP 2
+#endif
+constexpr int kBigGroup = RTMI_BIG_GROUP;  // sphere pairs per step of the big-sphere loop
 static_assert(kLeafMax >= 1 && kLeafMax <= 15, "leaf size");
 
 struct Accel {

@@ -39,6 +39,17 @@ class RtCamera(C.Structure):
     ]
 
 
+class RtNwCamera(C.Structure):
+    _fields_ = [("cam", RtCamera), ("time0", C.c_double), ("time1", C.c_double)]
+
+
+class RtNwFlat(C.Structure):
+    _fields_ = [(nm, C.c_int32) for nm in ("n_obj", "n_inst", "n_mat", "n_tex", "n_perlin", "n_image")] + [
+        (nm, _fp) for nm in ("obj", "inst", "mat", "tex", "perlin_vec")
+    ] + [("perlin_perm", _ip), ("image_desc", _ip), ("image_px", C.POINTER(C.c_uint8)), ("image_bytes", C.c_int64),
+         ("background", C.c_float * 3)]
+
+
 class RTError(RuntimeError):
     def __init__(self, what, code, msg):
         super().__init__(f"{what} failed: {ERRORS.get(code, code)}: {msg}")
@@ -89,6 +100,44 @@ SIGNATURES = {
     ),
     "rt_replay_worker": (C.c_int, [C.c_void_p, C.POINTER(RtCamera)] + [C.c_int32] * 5 + [_ip, _ip, _lp, _dp, _lp]),
     "rt_render_multi": (C.c_int, [C.POINTER(RtScene), C.POINTER(RtCamera)] + [C.c_int32] * 4 + [C.c_uint64, C.c_int32, _fp]),
+    # include/rtmi_nw.h (Next-Week renderer)
+    "rt_nw_camera_init": (C.c_int, [C.POINTER(RtNwCamera), _dp, _dp, _dp] + [C.c_double] * 6),
+    "rt_nw_scene_create": (C.c_int, [C.POINTER(C.c_void_p)]),
+    "rt_nw_scene_destroy": (C.c_int, [C.c_void_p]),
+    "rt_nw_tex_solid": (C.c_int, [C.c_void_p, C.c_double, C.c_double, C.c_double]),
+    "rt_nw_tex_checker": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    "rt_nw_tex_noise": (C.c_int, [C.c_void_p, C.c_double, _fp, _ip]),
+    "rt_nw_tex_image": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint8), C.c_int32, C.c_int32]),
+    "rt_nw_mat_lambertian": (C.c_int, [C.c_void_p, C.c_int32]),
+    "rt_nw_mat_metal": (C.c_int, [C.c_void_p, C.c_int32, C.c_double]),
+    "rt_nw_mat_dielectric": (C.c_int, [C.c_void_p, C.c_double]),
+    "rt_nw_mat_diffuse_light": (C.c_int, [C.c_void_p, C.c_int32]),
+    "rt_nw_mat_isotropic": (C.c_int, [C.c_void_p, C.c_int32]),
+    "rt_nw_sphere": (C.c_int, [C.c_void_p, _dp, C.c_double, C.c_int32]),
+    "rt_nw_moving_sphere": (C.c_int, [C.c_void_p, _dp, _dp, C.c_double, C.c_double, C.c_double, C.c_int32]),
+    "rt_nw_rect": (C.c_int, [C.c_void_p, C.c_int32] + [C.c_double] * 5 + [C.c_int32]),
+    "rt_nw_box": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int32]),
+    "rt_nw_constant_medium": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_int32]),
+    "rt_nw_medium_samples": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    "rt_nw_group": (C.c_int, [C.c_void_p, _ip, C.c_int32]),
+    "rt_nw_translate": (C.c_int, [C.c_void_p, C.c_int32, _dp]),
+    "rt_nw_rotate_y": (C.c_int, [C.c_void_p, C.c_int32, C.c_double]),
+    "rt_nw_world_add": (C.c_int, [C.c_void_p, C.c_int32]),
+    "rt_nw_set_background": (C.c_int, [C.c_void_p, C.c_double, C.c_double, C.c_double]),
+    "rt_nw_scene_preset": (
+        C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_uint8), C.c_int32, C.c_int32, C.c_double, C.c_uint32, C.POINTER(RtNwCamera)]),
+    "rt_nw_xorwow_uniforms": (C.c_int, [C.c_uint64, C.c_int32, _fp]),
+    "rt_nw_scene_flat": (C.c_int, [C.c_void_p, C.POINTER(RtNwFlat)]),
+    "rt_nw_ctx_create": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
+    "rt_nw_ctx_destroy": (C.c_int, [C.c_void_p]),
+    "rt_nw_ctx_set_scene": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "rt_nw_ctx_info": (C.c_int, [C.c_void_p, _ip, _ip]),
+    "rt_nw_render": (C.c_int, [C.c_void_p, C.POINTER(RtNwCamera)] + [C.c_int32] * 4 + [C.c_uint64, _fp]),
+    "rt_nw_render_rows": (
+        C.c_int,
+        [C.c_void_p, C.POINTER(RtNwCamera)] + [C.c_int32] * 4 + [C.c_uint64] + [C.c_int32] * 3 + [C.c_void_p, C.c_void_p],
+    ),
+    "rt_nw_ctx_last_segments": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
 }
 
 _lib = None

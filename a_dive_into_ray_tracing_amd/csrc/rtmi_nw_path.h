@@ -1,0 +1,566 @@
+// rtmi_nw_path.h — device-side Next-Week path tracing:
+// the reference's rt_next_week/cuda/ hittables, textures and materials as
+// float code with an explicit fmaf policy (-ffp-contract=off), restated
+// operation for operation by the CPU oracle (oracle/rt_nw_oracle.c), so the
+// kernel's images equal the oracle's bit for bit.  Transcendentals (sin,
+// log, atan2, acos) are our own polynomial evaluations for the same reason.
+// Semantics and deviations: DESIGN.md §9.2.
+#pragma once
+
+#include "rtmi_nw_types.h"
+#include "rtmi_path.h"
+
+namespace rtmi {
+namespace nw {
+
+using V = V3<float>;
+
+__device__ __forceinline__ V add3(V a, V b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V sub3(V a, V b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V mul3(V a, V b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ float dot3(V a, V b) { return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)); }
+// ray::at: o + t*d
+__device__ __forceinline__ V at3(V o, V d, float t) {
+  return mk(__builtin_fmaf(t, d.x, o.x), __builtin_fmaf(t, d.y, o.y), __builtin_fmaf(t, d.z, o.z));
+}
+
+// ---------------------------------------------------------------------------
+// transcendentals (mirrored by oracle/rt_nw_oracle.c)
+// ---------------------------------------------------------------------------
+// sin(x): quadrant k = rint(x * 2/pi), Cody-Waite reduction with a 3-part
+// pi/2 (fma: each product exact), then the Cephes sinf/cosf polynomials.
+__device__ __forceinline__ float nw_sinf(float x) {
+  const float kf = __builtin_rintf(x * 0.636619747f);
+  float r = __builtin_fmaf(-kf, 1.57079637f, x);
+  r = __builtin_fmaf(-kf, -4.37113883e-8f, r);
+  r = __builtin_fmaf(-kf, -1.77635684e-15f, r);
+  const int k = int(kf) & 3;
+  const float r2 = r * r;
+  float p = __builtin_fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f);
+  p = __builtin_fmaf(r2, p, -1.6666654611e-1f);
+  const float sn = __builtin_fmaf(r * r2, p, r);
+  float q = __builtin_fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+  q = __builtin_fmaf(r2, q, 4.166664568298827e-2f);
+  const float cs = __builtin_fmaf(r2 * r2, q, __builtin_fmaf(-0.5f, r2, 1.0f));
+  return k == 0 ? sn : k == 1 ? cs : k == 2 ? -sn : -cs;
+}
+
+// log(x), x > 0 normal: Cephes logf (x = m 2^e, m in [sqrt(.5), sqrt(2)))
+__device__ __forceinline__ float nw_logf(float x) {
+  const int bits = __float_as_int(x);
+  int e = ((bits >> 23) & 255) - 126;
+  float m = __int_as_float((bits & 0x7fffff) | 0x3f000000);  // [0.5, 1)
+  if (m < 0.707106781f) {
+    e -= 1;
+    m = m + m;
+  }
+  m = m - 1.0f;
+  const float z = m * m;
+  float y = __builtin_fmaf(7.0376836292e-2f, m, -1.1514610310e-1f);
+  y = __builtin_fmaf(y, m, 1.1676998740e-1f);
+  y = __builtin_fmaf(y, m, -1.2420140846e-1f);
+  y = __builtin_fmaf(y, m, 1.4249322787e-1f);
+  y = __builtin_fmaf(y, m, -1.6668057665e-1f);
+  y = __builtin_fmaf(y, m, 2.0000714765e-1f);
+  y = __builtin_fmaf(y, m, -2.4999993993e-1f);
+  y = __builtin_fmaf(y, m, 3.3333331174e-1f);
+  y = (y * m) * z;
+  const float fe = float(e);
+  y = __builtin_fmaf(fe, -2.12194440e-4f, y);
+  y = __builtin_fmaf(-0.5f, z, y);
+  return __builtin_fmaf(fe, 0.693359375f, m + y);
+}
+
+// atan(x): Cephes atanf
+__device__ __forceinline__ float nw_atanf(float x) {
+  const bool neg = x < 0.0f;
+  float a = neg ? -x : x, y0 = 0.0f;
+  if (a > 2.414213562373095f) {
+    y0 = 1.57079637f;
+    a = -1.0f / a;
+  } else if (a > 0.4142135623730950f) {
+    y0 = 0.785398185f;
+    a = (a - 1.0f) / (a + 1.0f);
+  }
+  const float z = a * a;
+  float p = __builtin_fmaf(8.05374449538e-2f, z, -1.38776856032e-1f);
+  p = __builtin_fmaf(p, z, 1.99777106478e-1f);
+  p = __builtin_fmaf(p, z, -3.33329491539e-1f);
+  const float r = __builtin_fmaf(p * z, a, a) + y0;
+  return neg ? -r : r;
+}
+__device__ __forceinline__ float nw_atan2f(float y, float x) {
+  if (x == 0.0f) return y > 0.0f ? 1.57079637f : y < 0.0f ? -1.57079637f : 0.0f;
+  const float a = nw_atanf(y / x);
+  if (x > 0.0f) return a;
+  return y >= 0.0f ? a + 3.14159274f : a - 3.14159274f;
+}
+__device__ __forceinline__ float nw_acosf(float x) {
+  x = __builtin_fminf(__builtin_fmaxf(x, -1.0f), 1.0f);
+  return nw_atan2f(__builtin_sqrtf((1.0f - x) * (1.0f + x)), x);
+}
+
+// ---------------------------------------------------------------------------
+// scene view
+// ---------------------------------------------------------------------------
+struct View {
+  const Obj *obj;  // non-media objects, BVH leaf order
+  const int32_t *obj_id;
+  const Obj *med;  // media, insertion order (evaluated before the BVH walk)
+  const int32_t *med_id;
+  int32_t nobj, nmed;
+  const Inst *inst;
+  const Mat *mat;
+  const Tex *tex;
+  const float4 *perlin_vec;
+  const int32_t *perlin_perm;
+  const uint8_t *image_px;
+  const Image *image;
+  const Node *nodes;
+  int32_t nnodes;
+  float bg[3];
+  int32_t has_media;
+};
+
+__device__ __forceinline__ float4 ld4(const float (&g)[4]) { return make_float4(g[0], g[1], g[2], g[3]); }
+
+// instance: world ray -> local ray (translate::hit hittable.h:66-69, then
+// rotate_y::hit hittable.h:147-156)
+__device__ __forceinline__ void to_local(const Inst &in, V &o, V &d) {
+  if (in.flags & 2) o = mk(o.x - in.off[0], o.y - in.off[1], o.z - in.off[2]);
+  if (in.flags & 1) {
+    o = mk(__builtin_fmaf(in.c, o.x, -(in.s * o.z)), o.y, __builtin_fmaf(in.s, o.x, in.c * o.z));
+    d = mk(__builtin_fmaf(in.c, d.x, -(in.s * d.z)), d.y, __builtin_fmaf(in.s, d.x, in.c * d.z));
+  }
+}
+// local point / normal -> world (rotate_y hittable.h:162-170, translate :75)
+__device__ __forceinline__ V rot_to_world(const Inst &in, V v) {
+  return mk(__builtin_fmaf(in.c, v.x, in.s * v.z), v.y, __builtin_fmaf(-in.s, v.x, in.c * v.z));
+}
+
+// ---------------------------------------------------------------------------
+// hittables, in the object's local frame; each returns whether a root in the
+// reference's interval exists and writes it (and the face of a box)
+// ---------------------------------------------------------------------------
+// sphere::hit sphere.h:42-77: disc > 0, roots strictly inside (t_min, t_max)
+__device__ __forceinline__ bool hit_sphere(V o, V d, V c, float r, float tmin, float tmax, float &t) {
+  const V oc = sub3(o, c);
+  const float a = dot3(d, d);
+  const float b = dot3(oc, d);
+  const float cc = dot3(oc, oc) - r * r;
+  const float disc = __builtin_fmaf(b, b, -(a * cc));
+  if (disc > 0.0f) {
+    const float sq = __builtin_sqrtf(disc);
+    float tt = (-b - sq) / a;
+    if (tt < tmax && tt > tmin) { t = tt; return true; }
+    tt = (-b + sq) / a;
+    if (tt < tmax && tt > tmin) { t = tt; return true; }
+  }
+  return false;
+}
+// moving_sphere::center moving_sphere.h:44-46
+__device__ __forceinline__ V moving_center(const Obj &ob, float time) {
+  const float f = (time - ob.g1[3]) / (ob.g2[0] - ob.g1[3]);
+  return mk(__builtin_fmaf(f, ob.g1[0] - ob.g0[0], ob.g0[0]), __builtin_fmaf(f, ob.g1[1] - ob.g0[1], ob.g0[1]),
+            __builtin_fmaf(f, ob.g1[2] - ob.g0[2], ob.g0[2]));
+}
+// moving_sphere::hit moving_sphere.h:48-77: disc >= 0, roots in [t_min, t_max]
+__device__ __forceinline__ bool hit_moving(V o, V d, V c, float r, float tmin, float tmax, float &t) {
+  const V oc = sub3(o, c);
+  const float a = dot3(d, d);
+  const float hb = dot3(oc, d);
+  const float cc = dot3(oc, oc) - r * r;
+  const float disc = __builtin_fmaf(hb, hb, -(a * cc));
+  if (disc < 0.0f) return false;
+  const float sq = __builtin_sqrtf(disc);
+  float root = (-hb - sq) / a;
+  if (root < tmin || tmax < root) {
+    root = (-hb + sq) / a;
+    if (root < tmin || tmax < root) return false;
+  }
+  t = root;
+  return true;
+}
+// xy_rect / xz_rect / yz_rect ::hit aarect.h:44-72, 103-131, 160-176.
+// axis k = plane normal axis, (a, b) = in-plane axes.
+template <int KA, int AA, int BA>
+__device__ __forceinline__ bool hit_rect(V o, V d, float a0, float a1, float b0, float b1, float k, float tmin,
+                                         float tmax, float &t) {
+  const float ok = KA == 0 ? o.x : KA == 1 ? o.y : o.z;
+  const float dk = KA == 0 ? d.x : KA == 1 ? d.y : d.z;
+  const float tt = (k - ok) / dk;
+  if (tt < tmin || tt > tmax) return false;
+  const float oa = AA == 0 ? o.x : o.y, da = AA == 0 ? d.x : d.y;
+  const float ob = BA == 1 ? o.y : o.z, db = BA == 1 ? d.y : d.z;
+  const float x = __builtin_fmaf(tt, da, oa);
+  const float y = __builtin_fmaf(tt, db, ob);
+  if (x < a0 || x > a1 || y < b0 || y > b1) return false;
+  t = tt;
+  return true;
+}
+__device__ __forceinline__ bool hit_rect_kind(int kind, V o, V d, const float4 g, float k, float tmin, float tmax,
+                                              float &t) {
+  if (kind == kRectXY) return hit_rect<2, 0, 1>(o, d, g.x, g.y, g.z, g.w, k, tmin, tmax, t);
+  if (kind == kRectXZ) return hit_rect<1, 0, 2>(o, d, g.x, g.y, g.z, g.w, k, tmin, tmax, t);
+  return hit_rect<0, 1, 2>(o, d, g.x, g.y, g.z, g.w, k, tmin, tmax, t);
+}
+// box::hit box.h:53-56 = hittable_list::hit over its six sides (box.h:37-50,
+// hittable_list.h:29-44): the shrinking closest_so_far makes a later side win
+// a tie.  Returns the face 0..5 in the reference's side order.
+__device__ __forceinline__ int hit_box(V o, V d, const float4 p0, const float4 p1, float tmin, float tmax, float &t) {
+  int face = -1;
+  float closest = tmax, tt;
+  if (hit_rect<2, 0, 1>(o, d, p0.x, p1.x, p0.y, p1.y, p1.z, tmin, closest, tt)) { closest = tt; face = 0; }
+  if (hit_rect<2, 0, 1>(o, d, p0.x, p1.x, p0.y, p1.y, p0.z, tmin, closest, tt)) { closest = tt; face = 1; }
+  if (hit_rect<1, 0, 2>(o, d, p0.x, p1.x, p0.z, p1.z, p1.y, tmin, closest, tt)) { closest = tt; face = 2; }
+  if (hit_rect<1, 0, 2>(o, d, p0.x, p1.x, p0.z, p1.z, p0.y, tmin, closest, tt)) { closest = tt; face = 3; }
+  if (hit_rect<0, 1, 2>(o, d, p0.y, p1.y, p0.z, p1.z, p1.x, tmin, closest, tt)) { closest = tt; face = 4; }
+  if (hit_rect<0, 1, 2>(o, d, p0.y, p1.y, p0.z, p1.z, p0.x, tmin, closest, tt)) { closest = tt; face = 5; }
+  t = closest;
+  return face;
+}
+
+// a medium's boundary (sphere, moving sphere or box) over (tmin, tmax)
+__device__ __forceinline__ bool hit_boundary(const Obj &ob, V o, V d, float time, float tmin, float tmax, float &t) {
+  const int bk = ob.aux & 255;
+  if (bk == kSphere) return hit_sphere(o, d, mk(ob.g0[0], ob.g0[1], ob.g0[2]), ob.g0[3], tmin, tmax, t);
+  if (bk == kMovingSphere) return hit_moving(o, d, moving_center(ob, time), ob.g0[3], tmin, tmax, t);
+  return hit_box(o, d, ld4(ob.g0), ld4(ob.g1), tmin, tmax, t) >= 0;
+}
+// constant_medium::hit constant_medium.h:41-78: entry t1 (clamped to 0) and
+// exit t2 of the boundary; the scattering distance -log(u)/density, drawn
+// `samples` times (the last that lands inside the boundary wins, DESIGN.md
+// §9.2).  The reference puts the scattering point at the entry t1
+// (constant_medium.h:73): make_rec recomputes it.
+__device__ __forceinline__ float medium_uniform(uint64_t seg_key, int32_t id, int s);
+__device__ __forceinline__ bool hit_medium(const Obj &ob, int32_t id, V o, V d, V dw, float time, uint64_t seg_key,
+                                           float &t) {
+  float r1, r2;
+  if (!hit_boundary(ob, o, d, time, -INFINITY, INFINITY, r1)) return false;
+  if (!hit_boundary(ob, o, d, time, float(double(r1) + 0.00001), INFINITY, r2)) return false;
+  if (r1 < 0.0f) r1 = 0.0f;
+  const float len = __builtin_sqrtf(dot3(dw, dw));
+  const float inside = (r2 - r1) * len;
+  const int samples = ob.aux >> 8;
+  bool hit = false;
+  for (int s = 0; s < samples; ++s) {
+    const float hd = ob.g2[3] * nw_logf(medium_uniform(seg_key, id, s));
+    if (!(hd > inside)) {
+      t = r1 + hd / len;
+      hit = true;
+    }
+  }
+  return hit;
+}
+
+// per-(segment, medium, sample) uniform in (0, 1]: a counter-based draw, so
+// no result depends on the order objects are visited in
+__device__ __forceinline__ float medium_uniform(uint64_t seg_key, int32_t id, int s) {
+  const uint64_t h = mix64(seg_key ^ (uint64_t(uint32_t(id) + 1u) * 0x9E3779B97F4A7C15ULL) ^
+                           (uint64_t(uint32_t(s)) * 0xD1B54A32D192ED03ULL));
+  return float(uint32_t(h >> 40) + 1u) * 0x1p-24f;
+}
+
+// One non-medium object's hit (world ray in; t_min = 0.001, no upper bound:
+// the caller applies the order-independent closest rule).  face: box side.
+__device__ __forceinline__ bool hit_object(const View &sc, const Obj &ob, V ow, V dw, float time, float &t,
+                                           int &face) {
+  V o = ow, d = dw;
+  if (ob.inst >= 0) to_local(sc.inst[ob.inst], o, d);
+  const float tmin = 0.001f;
+  switch (ob.kind) {
+    case kSphere: return hit_sphere(o, d, mk(ob.g0[0], ob.g0[1], ob.g0[2]), ob.g0[3], tmin, INFINITY, t);
+    case kMovingSphere: return hit_moving(o, d, moving_center(ob, time), ob.g0[3], tmin, INFINITY, t);
+    case kRectXY: case kRectXZ: case kRectYZ:
+      return hit_rect_kind(ob.kind, o, d, ld4(ob.g0), ob.g1[0], tmin, INFINITY, t);
+    default: face = hit_box(o, d, ld4(ob.g0), ld4(ob.g1), tmin, INFINITY, t); return face >= 0;
+  }
+}
+
+// Closest hit of a segment.  1. Media, in insertion order:
+// each one that hits is a candidate and sets its bit in the mask.  2. The
+// object BVH (global memory, stackless skip-link walk, slab test clipped to
+// [0, best_t]); an object whose twin medium hit is skipped.  The winner is
+// the smallest (t, insertion index) pair, so no result depends on the visit
+// order.  Returns the winner's index: [0, nobj) an object in leaf order,
+// nobj + m medium m; -1 none.
+__device__ __forceinline__ int32_t hit_world_nw(const View &sc, V o, V d, float time, uint64_t seg_key, float &best_t,
+                                                int &best_face) {
+  best_t = INFINITY;
+  int32_t best = -1, best_id = 0x7fffffff;
+  best_face = -1;
+  uint32_t med_hit = 0;
+  for (int32_t m = 0; m < sc.nmed; ++m) {
+    const Obj ob = sc.med[m];
+    const int32_t id = sc.med_id[m];
+    V lo = o, ld = d;
+    if (ob.inst >= 0) to_local(sc.inst[ob.inst], lo, ld);
+    float t;
+    if (hit_medium(ob, id, lo, ld, d, time, seg_key, t) && !(t < 0.001f)) {
+      med_hit |= 1u << m;
+      if (t < best_t || (t == best_t && id < best_id)) {
+        best_t = t;
+        best = sc.nobj + m;
+        best_id = id;
+      }
+    }
+  }
+  auto safe_inv = [](float v) { return 1.0f / (__builtin_fabsf(v) < 1e-20f ? __builtin_copysignf(1e-20f, v) : v); };
+  const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
+  const float ox = -o.x * ix, oy = -o.y * iy, oz = -o.z * iz;
+  int32_t node = 0;
+  while (node < sc.nnodes) {
+    const Node nd = sc.nodes[node];
+    const float tx0 = __builtin_fmaf(nd.bmin[0], ix, ox), tx1 = __builtin_fmaf(nd.bmax[0], ix, ox);
+    const float ty0 = __builtin_fmaf(nd.bmin[1], iy, oy), ty1 = __builtin_fmaf(nd.bmax[1], iy, oy);
+    const float tz0 = __builtin_fmaf(nd.bmin[2], iz, oz), tz1 = __builtin_fmaf(nd.bmax[2], iz, oz);
+    const float tnear = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx0, tx1), __builtin_fminf(ty0, ty1)),
+                                        __builtin_fmaxf(__builtin_fminf(tz0, tz1), 0.0f));
+    const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx0, tx1), __builtin_fmaxf(ty0, ty1)),
+                                       __builtin_fminf(__builtin_fmaxf(tz0, tz1), best_t));
+    const bool enter = tnear <= tfar;
+    if (enter && nd.leaf >= 0) {
+      const int32_t first = nd.leaf >> 4, cnt = nd.leaf & 15;
+      for (int32_t k = first; k < first + cnt; ++k) {
+        const Obj ob = sc.obj[k];
+        if (ob.aux > 0 && ((med_hit >> (ob.aux - 1)) & 1u)) continue;  // hidden by its medium
+        const int32_t id = sc.obj_id[k];
+        float t;
+        int face = -1;
+        if (hit_object(sc, ob, o, d, time, t, face) && (t < best_t || (t == best_t && id < best_id))) {
+          best_t = t;
+          best = k;
+          best_id = id;
+          best_face = face;
+        }
+      }
+    }
+    node = enter ? node + 1 : nd.skip;
+  }
+  return best;
+}
+
+// ---------------------------------------------------------------------------
+// textures (texture.h, perlin.h)
+// ---------------------------------------------------------------------------
+// perlin::noise perlin.h:30-63 + trilinear_interp perlin.h:114-127
+__device__ __forceinline__ float perlin_noise(const View &sc, int32_t pid, V p) {
+  const float4 *ranvec = sc.perlin_vec + pid * kPerlinN;
+  const int32_t *px = sc.perlin_perm + pid * 3 * kPerlinN, *py = px + kPerlinN, *pz = py + kPerlinN;
+  const float fx = __builtin_floorf(p.x), fy = __builtin_floorf(p.y), fz = __builtin_floorf(p.z);
+  float u = p.x - fx, v = p.y - fy, w = p.z - fz;
+  u = (u * u) * __builtin_fmaf(-2.0f, u, 3.0f);
+  v = (v * v) * __builtin_fmaf(-2.0f, v, 3.0f);
+  w = (w * w) * __builtin_fmaf(-2.0f, w, 3.0f);
+  const int i = int(fx), j = int(fy), k = int(fz);
+  float accum = 0.0f;
+#pragma unroll
+  for (int di = 0; di < 2; ++di)
+#pragma unroll
+    for (int dj = 0; dj < 2; ++dj)
+#pragma unroll
+      for (int dk = 0; dk < 2; ++dk) {
+        const float4 c = ranvec[px[(i + di) & 255] ^ py[(j + dj) & 255] ^ pz[(k + dk) & 255]];
+        const float wi = di ? u : 1.0f - u, wj = dj ? v : 1.0f - v, wk = dk ? w : 1.0f - w;
+        const float dd = dot3(mk(c.x, c.y, c.z), mk(u - float(di), v - float(dj), w - float(dk)));
+        accum = __builtin_fmaf((wi * wj) * wk, dd, accum);
+      }
+  return accum;
+}
+// perlin::turb perlin.h:65-78 (depth 7)
+__device__ __forceinline__ float perlin_turb(const View &sc, int32_t pid, V p) {
+  float accum = 0.0f, weight = 1.0f;
+  for (int i = 0; i < 7; ++i) {
+    accum = __builtin_fmaf(weight, perlin_noise(sc, pid, p), accum);
+    weight *= 0.5f;
+    p = mk(p.x * 2.0f, p.y * 2.0f, p.z * 2.0f);
+  }
+  return __builtin_fabsf(accum);
+}
+
+__device__ __forceinline__ V tex_leaf(const View &sc, const Tex &tx, float u, float v, V p) {
+  if (tx.kind == kSolid) return mk(tx.rgb[0], tx.rgb[1], tx.rgb[2]);
+  if (tx.kind == kNoise) {  // noise_texture::value texture.h:71-80 (marble)
+    const V sp = mk(tx.scale * p.x, tx.scale * p.y, tx.scale * p.z);
+    const float f = 0.5f * (1.0f + nw_sinf(__builtin_fmaf(10.0f, perlin_turb(sc, tx.a, sp), tx.scale * p.z)));
+    return mk(f, f, f);
+  }
+  // image_texture::value texture.h:94-120
+  const Image im = sc.image[tx.a];
+  if (im.w == 0) return mk(0.0f, 1.0f, 1.0f);
+  u = __builtin_fminf(__builtin_fmaxf(u, 0.0f), 1.0f);
+  v = 1.0f - __builtin_fminf(__builtin_fmaxf(v, 0.0f), 1.0f);
+  int i = int(u * float(im.w)), j = int(v * float(im.h));
+  if (i >= im.w) i = im.w - 1;
+  if (j >= im.h) j = im.h - 1;
+  i = (i + im.w / 2 + im.w / 3) % im.w;  // "try to shift the map" texture.h:110
+  const uint8_t *px = sc.image_px + im.offset + (j * im.w + i) * 3;
+  const float s = 1.0f / 255.0f;
+  return mk(s * float(px[0]), s * float(px[1]), s * float(px[2]));
+}
+// texture value; checker_texture::value texture.h:48-55 selects by the sign
+// of sin(10x) sin(10y) sin(10z)
+__device__ __forceinline__ V tex_value(const View &sc, int32_t tid, float u, float v, V p) {
+  Tex tx = sc.tex[tid];
+  if (tx.kind == kChecker) {
+    const float sines = (nw_sinf(10.0f * p.x) * nw_sinf(10.0f * p.y)) * nw_sinf(10.0f * p.z);
+    tx = sc.tex[sines < 0.0f ? tx.b : tx.a];
+  }
+  return tex_leaf(sc, tx, u, v, p);
+}
+__device__ __forceinline__ bool tex_needs_uv(const View &sc, int32_t tid) {
+  const Tex tx = sc.tex[tid];
+  if (tx.kind == kImage) return true;
+  if (tx.kind == kChecker) return sc.tex[tx.a].kind == kImage || sc.tex[tx.b].kind == kImage;
+  return false;
+}
+
+// sphere::get_sphere_uv sphere.h:30-40
+__device__ __forceinline__ void sphere_uv(V p, float &u, float &v) {
+  const float theta = nw_acosf(-p.y);
+  const float phi = nw_atan2f(-p.z, p.x) + 3.14159274f;
+  u = phi / (2.0f * 3.14159274f);
+  v = theta / 3.14159274f;
+}
+
+// ---------------------------------------------------------------------------
+// hit record of the winning object (deferred: recomputed once per segment)
+// ---------------------------------------------------------------------------
+struct Rec {
+  V p, n;
+  float u, v;
+  int32_t mat;
+};
+__device__ __forceinline__ Rec make_rec(const View &sc, const Obj &ob, V ow, V dw, float time, float t, int face) {
+  Rec r;
+  r.mat = ob.mat;
+  r.u = 0.0f;
+  r.v = 0.0f;
+  if (ob.kind == kMedium) {  // constant_medium.h:73-77: p at the entry point, arbitrary normal
+    V o = ow, d = dw;
+    const Inst in = ob.inst >= 0 ? sc.inst[ob.inst] : Inst{1.f, 0.f, {0.f, 0.f, 0.f}, 0, {0, 0}};
+    if (ob.inst >= 0) to_local(in, o, d);
+    float r1;
+    (void)hit_boundary(ob, o, d, time, -INFINITY, INFINITY, r1);
+    if (r1 < 0.0f) r1 = 0.0f;
+    r.p = at3(ow, dw, r1);
+    r.n = mk(1.0f, 0.0f, 0.0f);
+    return r;
+  }
+  V o = ow, d = dw;
+  Inst in{1.f, 0.f, {0.f, 0.f, 0.f}, 0, {0, 0}};
+  if (ob.inst >= 0) {
+    in = sc.inst[ob.inst];
+    to_local(in, o, d);
+  }
+  V p = at3(o, d, t), n;
+  const Mat mm = sc.mat[ob.mat];
+  const bool need_uv = mm.kind != kDielectric && tex_needs_uv(sc, mm.tex);
+  if (ob.kind == kSphere || ob.kind == kMovingSphere) {
+    const V c = ob.kind == kSphere ? mk(ob.g0[0], ob.g0[1], ob.g0[2]) : moving_center(ob, time);
+    const float inv_r = 1.0f / ob.g0[3];
+    n = mk(inv_r * (p.x - c.x), inv_r * (p.y - c.y), inv_r * (p.z - c.z));
+    if (need_uv) sphere_uv(n, r.u, r.v);
+  } else {
+    int kind = ob.kind;
+    float a0, a1, b0, b1;
+    if (kind == kBox) {  // box face -> its rect (box.h:37-48)
+      const float4 p0 = ld4(ob.g0), p1 = ld4(ob.g1);
+      kind = face < 2 ? kRectXY : face < 4 ? kRectXZ : kRectYZ;
+      if (kind == kRectXY) { a0 = p0.x; a1 = p1.x; b0 = p0.y; b1 = p1.y; }
+      else if (kind == kRectXZ) { a0 = p0.x; a1 = p1.x; b0 = p0.z; b1 = p1.z; }
+      else { a0 = p0.y; a1 = p1.y; b0 = p0.z; b1 = p1.z; }
+    } else {
+      a0 = ob.g0[0]; a1 = ob.g0[1]; b0 = ob.g0[2]; b1 = ob.g0[3];
+    }
+    // u, v from the in-plane hit coordinates (aarect.h:59-60, 119-120, 170-171)
+    float x, y;
+    if (kind == kRectXY) { x = __builtin_fmaf(t, d.x, o.x); y = __builtin_fmaf(t, d.y, o.y); n = mk(0.f, 0.f, 1.f); }
+    else if (kind == kRectXZ) { x = __builtin_fmaf(t, d.x, o.x); y = __builtin_fmaf(t, d.z, o.z); n = mk(0.f, 1.f, 0.f); }
+    else { x = __builtin_fmaf(t, d.y, o.y); y = __builtin_fmaf(t, d.z, o.z); n = mk(1.f, 0.f, 0.f); }
+    r.u = (x - a0) / (a1 - a0);
+    r.v = (y - b0) / (b1 - b0);
+  }
+  if (in.flags & 1) {
+    p = rot_to_world(in, p);
+    n = rot_to_world(in, n);
+  }
+  if (in.flags & 2) p = mk(p.x + in.off[0], p.y + in.off[1], p.z + in.off[2]);
+  r.p = p;
+  r.n = n;
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// materials (rt_next_week/cuda/material.h)
+// ---------------------------------------------------------------------------
+// schlick material.h:97-101
+__device__ __forceinline__ float schlick(float cosine, float ri) {
+  float r0 = (1.0f - ri) / (1.0f + ri);
+  r0 = r0 * r0;
+  return __builtin_fmaf(1.0f - r0, pow5(1.0f - cosine), r0);
+}
+// Returns true if the ray scattered (dir, atten set); emitted light is
+// handled by the caller.
+__device__ __forceinline__ bool scatter_nw(const View &sc, const Rec &rec, V din, Xoro &g, V &atten, V &dir) {
+  const Mat m = sc.mat[rec.mat];
+  switch (m.kind) {
+    case kLambertian: {  // material.h:45-55: target = p + n + random_in_unit_sphere
+      const V rs = in_sphere_direct(g);
+      const V target = add3(add3(rec.p, rec.n), rs);
+      dir = sub3(target, rec.p);
+      atten = tex_value(sc, m.tex, rec.u, rec.v, rec.p);
+      return true;
+    }
+    case kMetal: {  // material.h:72-86
+      const V refl = reflect<true>(unit<true>(din), rec.n);
+      const V rs = in_sphere_direct(g);
+      dir = mk(__builtin_fmaf(m.fuzz, rs.x, refl.x), __builtin_fmaf(m.fuzz, rs.y, refl.y),
+               __builtin_fmaf(m.fuzz, rs.z, refl.z));
+      atten = tex_value(sc, m.tex, rec.u, rec.v, rec.p);
+      return dot3(dir, rec.n) > 0.0f;
+    }
+    case kDielectric: {  // material.h:119-148 (+ refract :103-114)
+      const V n = rec.n;
+      const V reflected = reflect<true>(din, n);
+      atten = mk(1.0f, 1.0f, 1.0f);
+      const float dn = dot3(din, n);
+      const float dlen = __builtin_sqrtf(dot3(din, din));
+      V outward;
+      float ni, cosine;
+      if (dn > 0.0f) {
+        outward = mk(-n.x, -n.y, -n.z);
+        ni = m.ir;
+        cosine = dn / dlen;
+        cosine = __builtin_sqrtf(1.0f - (m.ir * m.ir) * __builtin_fmaf(-cosine, cosine, 1.0f));
+      } else {
+        outward = n;
+        ni = 1.0f / m.ir;
+        cosine = -dn / dlen;
+      }
+      const V uv = unit<true>(din);
+      const float dt = dot3(uv, outward);
+      const float disc = 1.0f - (ni * ni) * __builtin_fmaf(-dt, dt, 1.0f);
+      V refracted = mk(0.f, 0.f, 0.f);
+      float reflect_prob = 1.0f;
+      if (disc > 0.0f) {
+        const float sq = __builtin_sqrtf(disc);
+        refracted = mk(__builtin_fmaf(-outward.x, sq, ni * __builtin_fmaf(-outward.x, dt, uv.x)),
+                       __builtin_fmaf(-outward.y, sq, ni * __builtin_fmaf(-outward.y, dt, uv.y)),
+                       __builtin_fmaf(-outward.z, sq, ni * __builtin_fmaf(-outward.z, dt, uv.z)));
+        reflect_prob = schlick(cosine, m.ir);
+      }
+      dir = g.uni() < reflect_prob ? reflected : refracted;
+      return true;
+    }
+    case kIsotropic: {  // material.h:180-190
+      dir = in_sphere_direct(g);
+      atten = tex_value(sc, m.tex, rec.u, rec.v, rec.p);
+      return true;
+    }
+    default: return false;  // diffuse_light material.h:159-177
+  }
+}
+
+}  // namespace nw
+}  // namespace rtmi

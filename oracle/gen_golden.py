@@ -18,6 +18,9 @@ Fixtures (all produced by the reference's own functions, see ref_harness.cpp):
   learn_400x225x100.ppm               config 1 oracle image (reference P3 re-encoded as P6)
   gallery_final.png                   /root/reference/gallery/final.png (config 2, CPU oracle output)
   gallery_final_tiles40.npy           40x40 tile means of that PNG (float64, [20,30,3])
+  gallery_final_scene_5000.png        /root/reference/gallery/final_scene_5000.png (the Next-Week final
+                                      scene, the CUDA reference's output; statistical golden for rtmi_nw)
+  earthmap.jpeg                       /root/reference/rt_next_week/cuda/earthmap.jpeg (its earth texture)
 """
 import hashlib
 import os
@@ -89,6 +92,9 @@ def main():
     h, w, _ = img.shape
     tiles = img.reshape(h // 40, 40, w // 40, 40, 3).mean(axis=(1, 3))
     np.save(os.path.join(GOLD, "gallery_final_tiles40.npy"), tiles)
+    # Next-Week data files: the reference's own render and texture
+    shutil.copyfile("/root/reference/gallery/final_scene_5000.png", os.path.join(GOLD, "gallery_final_scene_5000.png"))
+    shutil.copyfile("/root/reference/rt_next_week/cuda/earthmap.jpeg", os.path.join(GOLD, "earthmap.jpeg"))
     print("golden vectors written to", GOLD)
 
 

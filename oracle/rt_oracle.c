@@ -463,3 +463,4 @@ int32_t or_fast_sample(const or_scene *s, const or_camera *c, int32_t W, int32_t
   free(w.s);
   return (int32_t)segs;
 }
+#include "rt_nw_oracle.inc"

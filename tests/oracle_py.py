@@ -184,3 +184,66 @@ def load_camera_txt(path):
         vals = [float(x) for x in t[1:]]
         out[t[0]] = vals if len(vals) > 1 else vals[0]
     return out
+
+
+# ---- Next-Week restatement (oracle/rt_nw_oracle.inc) ----------------------
+class OrNwScene(C.Structure):
+    _fields_ = [("n_obj", C.c_int32), ("n_inst", C.c_int32)] + [
+        (nm, _fp) for nm in ("obj", "inst", "mat", "tex", "perlin_vec")
+    ] + [("perlin_perm", _ip), ("image_desc", _ip), ("image_px", C.POINTER(C.c_uint8)), ("bg", C.c_float * 3)]
+
+
+def _nw_bind():
+    L = lib()
+    if not getattr(L, "_nw_bound", False):
+        L.or_nw_render.argtypes = [C.POINTER(OrNwScene), C.POINTER(OrCamera), C.c_double, C.c_double] + [C.c_int32] * 4 + [
+            C.c_uint64] + [C.c_int32] * 3 + [_fp, _lp]
+        L.or_nw_render.restype = C.c_int32
+        L.or_nw_math.argtypes = [C.c_int32, C.c_int32, _fp, _fp]
+        L._nw_bound = True
+    return L
+
+
+def nw_scene(flat):
+    """OrNwScene over the arrays of nextweek.Scene.flat() (kept alive on the struct)."""
+    keep = {k: (np.ascontiguousarray(v) if isinstance(v, np.ndarray) else v) for k, v in flat.items()}
+    for k in ("obj", "inst", "mat", "tex", "perlin_vec", "perlin_perm", "image_desc", "image_px"):
+        if keep[k].size == 0:
+            keep[k] = np.zeros(16, keep[k].dtype)
+    s = OrNwScene()
+    s.n_obj = int(flat["n_obj"])
+    s.n_inst = int(flat["inst"].size // 8)
+    for k in ("obj", "inst", "mat", "tex", "perlin_vec"):
+        setattr(s, k, keep[k].ctypes.data_as(_fp))
+    s.perlin_perm = keep["perlin_perm"].ctypes.data_as(_ip)
+    s.image_desc = keep["image_desc"].ctypes.data_as(_ip)
+    s.image_px = keep["image_px"].ctypes.data_as(C.POINTER(C.c_uint8))
+    for c in range(3):
+        s.bg[c] = float(flat["background"][c])
+    s._keep = keep
+    return s
+
+
+def nw_render(flat, nwcam, W, H, spp, depth, seed, row0=0, row_step=1, nrows=None):
+    """Oracle image (sums) + world.hit count for rows row0 + r*row_step of a W x H Next-Week render."""
+    L = _nw_bind()
+    nrows = H if nrows is None else nrows
+    s = nw_scene(flat)
+    cam = OrCamera()
+    C.memmove(C.byref(cam), C.byref(nwcam.cam), C.sizeof(cam))
+    out = np.zeros(nrows * W * 3, np.float32)
+    segs = C.c_int64()
+    rc = L.or_nw_render(C.byref(s), C.byref(cam), nwcam.time0, nwcam.time1, W, H, spp, depth, seed, row0, row_step,
+                        nrows, out.ctypes.data_as(_fp), C.byref(segs))
+    if rc != 0:
+        raise ValueError("or_nw_render failed")
+    return out.reshape(nrows, W, 3), segs.value
+
+
+def nw_math(fn, x):
+    L = _nw_bind()
+    x = np.ascontiguousarray(x, np.float32)
+    n = x.size // 2 if fn == 2 else x.size
+    out = np.zeros(n, np.float32)
+    L.or_nw_math(fn, n, x.ctypes.data_as(_fp), out.ctypes.data_as(_fp))
+    return out

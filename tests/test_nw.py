@@ -1,0 +1,182 @@
+"""Next-Week renderer, CPU side: the scene builder and
+flattening (include/rtmi_nw.h), the curand XORWOW restatement behind the
+reference's scene generator, the reference scenes' structure
+(rt_next_week/cuda/main.cu:163-413), and the oracle's transcendentals.
+
+Parity status: the CUDA reference cannot run here, so the XORWOW stream and
+scene contents are pinned by an independent Python restatement of cuRAND's
+published generator plus the scene structure the reference code spells out;
+the GPU kernel is pinned bit-exactly to the oracle (tests/test_nw_gpu.py)
+and statistically to the reference's own render (gallery/final_scene_5000.png).
+"""
+import math
+import os
+from fractions import Fraction
+
+import numpy as np
+import pytest
+
+import a_dive_into_ray_tracing_amd.nextweek as nw
+import oracle_py as O
+
+GOLD = O.GOLDEN
+
+
+def _f32_round(x: Fraction) -> np.float32:
+    """Correctly rounded (nearest-even) float32 of an exact rational."""
+    f = np.float32(float(x))
+    lo, hi = (f, np.nextafter(f, np.float32(np.inf))) if Fraction(float(f)) <= x else (np.nextafter(f, np.float32(-np.inf)), f)
+    dl, dh = x - Fraction(float(lo)), Fraction(float(hi)) - x
+    if dl < dh:
+        return lo
+    if dh < dl:
+        return hi
+    return lo if (lo.view(np.uint32) & 1) == 0 else hi
+
+
+def _xorwow_py(seed, n):
+    """cuRAND XORWOW, restated independently: curand_init(seed, 0, 0) then
+    curand_uniform = fma(float(x), 2^-32 (as float), 2^-33)."""
+    M = 0xFFFFFFFF
+    s0 = (seed & M) ^ 0xAAD26B49
+    s1 = (seed >> 32) ^ 0xF7DCEFDD
+    t0 = (1099087573 * s0) & M
+    t1 = (2591861531 * s1) & M
+    d = (6615241 + t1 + t0) & M
+    v = [(123456789 + t0) & M, 362436069 ^ t0, (521288629 + t1) & M, 88675123 ^ t1, (5783321 + t0) & M]
+    inv = Fraction(float(np.float32(2.3283064e-10)))
+    out = []
+    for _ in range(n):
+        t = v[0] ^ (v[0] >> 2)
+        v = v[1:] + [((v[4] ^ ((v[4] << 4) & M)) ^ (t ^ ((t << 1) & M))) & M]
+        d = (d + 362437) & M
+        x = (v[4] + d) & M
+        out.append(_f32_round(Fraction(float(np.float32(x))) * inv + inv / 2))
+    return np.array(out, np.float32)
+
+
+def test_xorwow_matches_independent_restatement():
+    got = nw.xorwow_uniforms(3000, seed=1984)
+    want = _xorwow_py(1984, 3000)
+    assert np.array_equal(got, want)
+    assert (got > 0).all() and (got <= 1).all()
+    assert abs(got.mean() - 0.5) < 0.02
+
+
+def _kinds(f):
+    return f["obj"].reshape(-1, 16)[:, 12:16].copy().view(np.int32)
+
+
+def test_final_scene_structure():
+    """rt_next_week_final_scene main.cu:331-413: 400 ground boxes with heights
+    random_float(1, 101) in draw order, a light, 4 spheres, 2 media, earth,
+    marble sphere, and 1000 cluster spheres under translate(rotate_y(15))."""
+    img = nw.load_image(os.path.join(GOLD, "earthmap.jpeg"))
+    s, cam = nw.preset("final", image=img, aspect=1.0)
+    f = s.flat()
+    assert f["n_obj"] == 1409
+    k = _kinds(f)
+    obj = f["obj"].reshape(-1, 16)
+    assert (k[:400, 0] == 5).all()  # boxes
+    u = _xorwow_py(1984, 400)
+    y1 = np.array([_f32_round(Fraction(float(x)) * 100 + 1) for x in u], np.float32)
+    assert np.array_equal(obj[:400, 5], y1)  # g1.y = box top
+    assert np.array_equal(obj[:400, 0], np.repeat(np.arange(-1000, 1000, 100, dtype=np.float32), 20))
+    assert (obj[:400, 1] == 0).all()
+    assert list(k[400:409, 0]) == [3, 1, 0, 0, 0, 6, 6, 0, 0]  # xz light, moving, 3 spheres, 2 media, earth, marble
+    assert (k[409:, 0] == 0).all() and (obj[409:, 3] == 10).all()
+    assert (k[409:, 2] == 0).all() and (k[:409, 2] == -1).all()  # one shared instance for the cluster
+    inst = f["inst"].reshape(-1, 8)
+    assert inst.shape[0] == 1
+    assert inst[0, 0] == np.float32(math.cos(math.radians(15))) and inst[0, 1] == np.float32(math.sin(math.radians(15)))
+    assert list(inst[0, 2:5]) == [-100, 270, 395]
+    cl = obj[409:, :3]
+    assert cl.min() >= 0 and cl.max() <= 165
+    # media: fog (r 5000, density 1e-4) and the blue sphere's interior (density 0.2)
+    med = obj[k[:, 0] == 6]
+    assert sorted(med[:, 3].tolist()) == [70, 5000]
+    assert np.allclose(sorted(-1.0 / med[:, 11].astype(np.float64)), [0.0001, 0.2], rtol=1e-6)
+    # the fog takes two scattering-distance samples (the reference's span-1 BVH leaf);
+    # the glass sphere at 404 is the blue medium's (405) boundary: its twin
+    assert k[405, 3] == (0 | 1 << 8) and k[406, 3] == (0 | 2 << 8)
+    assert k[404, 3] == 405 + 1 and (np.delete(k[:409, 3], [404, 405, 406]) == 0).all()
+    assert list(f["background"]) == [0, 0, 0]
+    assert tuple(np.round(cam.cam.origin, 6)) == (478, 278, -600)
+
+
+def test_cornell_instances_and_media():
+    s, _ = nw.preset("cornell_smoke", aspect=1.0)
+    f = s.flat()
+    k = _kinds(f)
+    assert list(k[:, 0]) == [4, 4, 3, 3, 3, 2, 6, 6]
+    assert list(k[6:, 3] & 255) == [5, 5] and list(k[6:, 3] >> 8) == [1, 1]  # media over boxes, one sample
+    assert (k[:6, 3] == 0).all()  # no twins: the boxes are not in the world themselves
+    inst = f["inst"].reshape(-1, 8)
+    assert inst.shape[0] == 2
+    for row, ang, off in zip(inst, (15, -18), ((265, 0, 295), (130, 0, 65))):
+        assert row[0] == np.float32(math.cos(math.radians(ang))) and row[1] == np.float32(math.sin(math.radians(ang)))
+        assert tuple(row[2:5]) == off
+        assert row[5:6].view(np.int32)[0] == 3
+
+
+def test_perlin_tables_are_permutations():
+    s, _ = nw.preset("two_perlin_spheres", aspect=1.0)
+    f = s.flat()
+    perm = f["perlin_perm"].reshape(3, 256)
+    for p in perm:
+        assert sorted(p.tolist()) == list(range(256))
+    rv = f["perlin_vec"].reshape(256, 4)
+    assert (np.abs(rv[:, :3]) <= 1).all() and (rv[:, 3] == 0).all()
+    # ranvec = random_vec3(-1, 1) from the stream after nothing else was drawn
+    u = _xorwow_py(1984, 3)
+    assert np.array_equal(rv[0, :3], np.array([_f32_round(Fraction(float(x)) * 2 - 1) for x in u], np.float32))
+
+
+def test_transform_composition():
+    """rotate_y(translate(x)) composes into one instance: offset rotated."""
+    s = nw.Scene()
+    m = s.lambertian(s.solid(1, 1, 1))
+    b = s.rotate_y(s.translate(s.box((0, 0, 0), (1, 1, 1), m), (10, 0, 0)), 90)
+    s.add(b)
+    inst = s.flat()["inst"].reshape(-1, 8)[0]
+    assert abs(inst[0]) < 1e-7 and inst[1] == 1
+    # world = R(90) (x + (10,0,0)): R maps x -> -z for 90 degrees (rotate_y's c x + s z, -s x + c z)
+    assert abs(inst[2]) < 1e-6 and inst[3] == 0 and inst[4] == -10
+
+
+def test_builder_errors():
+    s = nw.Scene()
+    with pytest.raises(Exception):
+        s.lambertian(3)  # no such texture
+    t = s.solid(1, 0, 0)
+    ch = s.checker(t, t)
+    with pytest.raises(Exception):
+        s.checker(ch, t)  # nested checker
+    m = s.lambertian(t)
+    r = s.rect("xy", 0, 1, 0, 1, 0, m)
+    with pytest.raises(Exception):
+        s.constant_medium(r, 0.1, t)  # rect boundary: flatten fails
+        s.add(s.constant_medium(r, 0.1, t))
+        s.flat()
+    with pytest.raises(Exception):
+        nw.camera((0, 0, 0), (0, 0, -1), (0, 1, 0), 40, 1, 0, 1, 0.5, 2.0)  # shutter outside [0, 1]
+
+
+def test_oracle_transcendentals():
+    x = np.linspace(-300, 300, 200001).astype(np.float32)
+    assert np.abs(O.nw_math(0, x) - np.sin(x.astype(np.float64))).max() < 2e-6
+    u = np.concatenate([np.arange(1, 1 << 12, dtype=np.float32), np.linspace(1, 1 << 24, 100000, dtype=np.float32)]) * np.float32(2**-24)
+    assert np.abs(O.nw_math(1, u) - np.log(u.astype(np.float64))).max() < 3e-6
+    rng = np.random.default_rng(1)
+    yx = rng.normal(size=(50000, 2)).astype(np.float32)
+    assert np.abs(O.nw_math(2, yx) - np.arctan2(yx[:, 0].astype(np.float64), yx[:, 1])).max() < 1e-6
+    c = np.linspace(-1, 1, 100001).astype(np.float32)
+    assert np.abs(O.nw_math(3, c) - np.arccos(c.astype(np.float64))).max() < 2e-6
+
+
+def test_oracle_presets_render_finite():
+    img = nw.load_image(os.path.join(GOLD, "earthmap.jpeg"))
+    for which in range(1, 9):
+        s, cam = nw.preset(which, image=img, aspect=1.0)
+        out, segs = O.nw_render(s.flat(), cam, 8, 8, 2, 50, 1984)
+        assert np.isfinite(out).all() and (out >= 0).all() and segs >= 8 * 8 * 2

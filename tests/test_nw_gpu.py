@@ -1,0 +1,114 @@
+"""Next-Week renderer on the GPU: the gfx950 kernel
+(librtmi.so rt_nw_*) against the CPU oracle (oracle/rt_nw_oracle.inc).
+
+  * bit-exact: every reference scene (create_world cases 1-8), ragged sizes,
+    strips and chunked accumulation give the oracle's sums bit for bit and
+    the same world.hit count — the GPU's object BVH and leaf order against
+    the oracle's brute-force list;
+  * statistics: the final scene (main.cu:331-413) at the reference's
+    800x800 against the reference's own 5000-spp render,
+    gallery/final_scene_5000.png (tests/golden/), by 50x50-pixel tile means.
+"""
+import os
+import time
+
+import numpy as np
+import pytest
+
+import a_dive_into_ray_tracing_amd.nextweek as nw
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+GOLD = O.GOLDEN
+SEED = 1984
+
+
+@pytest.fixture(scope="module")
+def earth():
+    return nw.load_image(os.path.join(GOLD, "earthmap.jpeg"))
+
+
+@pytest.mark.parametrize("which", list(range(1, 9)))
+def test_presets_bit_exact_vs_oracle(which, earth):
+    W, H, spp = 29, 23, 3  # ragged: partial 8x8 tiles on both axes
+    s, cam = nw.preset(which, image=earth, aspect=W / H)
+    r = nw.NwRenderer(s)
+    got = r.render(cam, W, H, spp, 50, SEED)
+    segs = r.last_segments()
+    r.close()
+    want, want_segs = O.nw_render(s.flat(), cam, W, H, spp, 50, SEED)
+    assert np.isfinite(got).all()
+    assert np.array_equal(got, want), f"scene {which}: max |d| {np.abs(got - want).max()}"
+    assert segs == want_segs
+
+
+@pytest.mark.parametrize("which", [6, 7, 8])
+def test_chunked_strips_bit_exact(which, earth):
+    """spp > the 32-sample item (two-item accumulation + finalize) and an
+    interleaved strip of rows, through rt_nw_render_rows on a torch stream."""
+    import torch
+
+    W, H, spp = 24, 40, 70
+    s, cam = nw.preset(which, image=earth, aspect=1.0)
+    r = nw.NwRenderer(s)
+    row0, step, nrows = 1, 3, 14  # rows 1, 4, ..., 40 (the last past H: zero)
+    strip = torch.full((nrows, W, 3), -1.0, dtype=torch.float32, device="cuda")
+    st = torch.cuda.Stream()
+    r.render_rows(cam, W, H, spp, 50, SEED, row0, step, nrows, strip.data_ptr(), st.cuda_stream)
+    st.synchronize()
+    got = strip.cpu().numpy()
+    r.close()
+    want, _ = O.nw_render(s.flat(), cam, W, H, spp, 50, SEED, row0=row0, row_step=step, nrows=13)
+    assert np.array_equal(got[:13], want)
+    assert (got[13] == 0).all()
+
+
+def test_depth_limit_returns_background(earth):
+    """max_depth 1: every path that scatters once returns the background
+    (main.cu:100); sky scenes show it."""
+    s, cam = nw.preset(2, aspect=1.0)  # two_spheres, sky background
+    r = nw.NwRenderer(s)
+    got = r.render(cam, 16, 16, 4, 1, SEED)
+    r.close()
+    want, _ = O.nw_render(s.flat(), cam, 16, 16, 4, 1, SEED)
+    assert np.array_equal(got, want)
+
+
+def _png(path):
+    from PIL import Image
+
+    return np.asarray(Image.open(path).convert("RGB"), dtype=np.float64)
+
+
+def _quantize(sums, spp):
+    """main.cu:563-575 (255.99 * sqrt(mean), clamped to a byte as a PNG holds it), top row first."""
+    c = np.sqrt(np.clip(sums / spp, 0, None))
+    return np.clip(np.floor(255.99 * c), 0, 255)[::-1]
+
+
+def test_final_scene_statistics_vs_reference_gallery(earth):
+    """The final scene at 800x800 (main.cu:520-523) vs the reference's own
+    render at 5000 spp, by 50x50-pixel tile means (printed for the record).
+    What remains is our 1024-spp noise and the deviations of DESIGN.md §9.2
+    (our sample stream vs per-pixel curand, the JPEG decoder)."""
+    W = H = 800
+    spp = 1024
+    s, cam = nw.preset("final", image=earth, aspect=1.0)
+    r = nw.NwRenderer(s)
+    t0 = time.time()
+    img = r.render(cam, W, H, spp, 50, SEED)
+    dt = time.time() - t0
+    segs = r.last_segments()
+    r.close()
+    ours = _quantize(img, spp)
+    ref = _png(os.path.join(GOLD, "gallery_final_scene_5000.png"))
+    d = ours - ref
+    to = ours.reshape(16, 50, 16, 50, 3).mean(axis=(1, 3))
+    tr = ref.reshape(16, 50, 16, 50, 3).mean(axis=(1, 3))
+    td = np.abs(to - tr)
+    print(f"nw final 800x800x{spp}: {dt:.2f} s, {W * H * spp / dt / 1e6:.0f} Msamples/s, {segs / (W * H * spp):.3f} seg/sample; "
+          f"vs gallery: bias {d.mean():.3f} MAE {np.abs(d).mean():.3f} tile MAE {td.mean():.3f} tile max {td.max():.2f} "
+          f"tile p95 {np.percentile(td, 95):.2f}")
+    # measured at 1024 spp: bias -0.55, tile MAE 0.59 (before the medium rules of
+    # bias -12.7, tile MAE 12.9)
+    assert abs(d.mean()) < 1.0 and td.mean() < 1.0 and td.max() < 6

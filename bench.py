@@ -27,6 +27,12 @@ untimed launch of the same rows.
 cpu_baseline: the reference itself (oracle/_ref/ref_harness: worker() at -O2,
 16 std::threads as the reference's concurrency) on a bounded sample, rank 0,
 N = 1 only.
+
+--workload selects a secondary line (not the headline): nw_motion_blur = the
+Next-Week random scene with moving spheres at 1200x800x500 (the reference's
+only published Next-Week number, rt_next_week/cuda/README.md:167-174: 37.88 s),
+nw_final = the Next-Week final scene at 800x800 (main.cu:517-524; --nw-spp,
+default 1024).  Same row partition and gather as the headline.
 """
 import argparse
 import json
@@ -95,9 +101,13 @@ def main():
                     help="closest-hit search: bvh (default; same image bit for bit) or brute force")
     ap.add_argument("--ordering", choices=["cost", "none"], default="cost")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=["config2", "nw_motion_blur", "nw_final"], default="config2")
+    ap.add_argument("--nw-spp", type=int, default=0, help="spp of the nw_* workloads (default: 500 / 1024)")
     ap.add_argument("--strip-of", type=int, default=0,
                     help="analysis only: time ONE rank's interleaved strip of an N-GPU run on this GPU")
     args = ap.parse_args()
+    if args.workload != "config2":
+        return bench_nw(args)
 
     import torch
     import torch.distributed as dist
@@ -253,6 +263,96 @@ def main():
         }
         if N == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(line), flush=True)
+    r.close()
+    if N > 1:
+        dist.destroy_process_group()
+
+
+NW_PUBLISHED_MSPS = 1200 * 800 * 500 / 37.8792 / 1e6  # rt_next_week/cuda/README.md:167-174 (RTX 2060 Max-Q)
+
+
+def bench_nw(args):
+    """Secondary line: a Next-Week scene (include/rtmi_nw.h) with the headline's
+    timing contract (barrier + sync around K steps, max over ranks)."""
+    import torch
+    import torch.distributed as dist
+
+    import a_dive_into_ray_tracing_amd.nextweek as nw
+    from a_dive_into_ray_tracing_amd import dist as rdist
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    N = world_size
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if N > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    if args.workload == "nw_motion_blur":
+        which, Wn, Hn, spp = 1, 1200, 800, args.nw_spp or 500
+        earth = None
+    else:
+        which, Wn, Hn, spp = 8, 800, 800, args.nw_spp or 1024
+        earth = nw.load_image(os.path.join(REPO, "tests", "golden", "earthmap.jpeg"))
+    scene, cam = nw.preset(which, image=earth, aspect=Wn / Hn)
+    r = nw.NwRenderer(scene, local_rank)
+    row0, row_step, nrows = rdist.strip_rows(Hn, rank, N)
+    strip = torch.empty((nrows, Wn, 3), dtype=torch.float32, device=dev)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    ev = []
+
+    def step(record):
+        if record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        r.render_rows(cam, Wn, Hn, spp, DEPTH, SEED, row0, row_step, nrows, strip.data_ptr(), stream.cuda_stream)
+        if record:
+            e1.record(stream)
+            ev.append((e0, e1))
+        if N > 1:
+            rdist.gather_strips(strip, rank, N, dst=0)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    if N > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    if N > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if N > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    segs = r.last_segments()
+    if rank == 0:
+        samples = Wn * Hn * spp
+        value = samples * args.steps / elapsed / 1e6
+        line = {
+            "metric": f"Msamples/sec (pixels x spp) on the Next-Week {args.workload[3:]} scene",
+            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": N, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": round(value / NW_PUBLISHED_MSPS, 1) if args.workload == "nw_motion_blur" and spp == 500 else None,
+            "dtype": "f32",
+            "data": "synthetic: the reference's scene regenerated from a restated curand XORWOW (curand_init(1984,0,0))",
+            "config": {"workload": f"{args.workload}_{Wn}x{Hn}_{spp}spp_depth{DEPTH}", "scene": which, "width": Wn,
+                       "height": Hn, "spp": spp, "max_depth": DEPTH, "seed": SEED,
+                       "partition": "interleaved rows, one RCCL gather" if N > 1 else "single GPU"},
+            "roofline": None,
+            "kernel_ms": round(kernel_ms, 3),
+            "segments_per_sample_rank0": round(segs / (nrows * Wn * spp), 4),
+            "vs_baseline_ref": "reference rt_next_week CUDA, random_scene with moving spheres 1200x800x500 in 37.88 s "
+                               "(RTX 2060 Max-Q): 12.67 Msamples/s",
+        }
         print(json.dumps(line), flush=True)
     r.close()
     if N > 1:

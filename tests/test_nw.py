@@ -180,3 +180,14 @@ def test_oracle_presets_render_finite():
         s, cam = nw.preset(which, image=img, aspect=1.0)
         out, segs = O.nw_render(s.flat(), cam, 8, 8, 2, 50, 1984)
         assert np.isfinite(out).all() and (out >= 0).all() and segs >= 8 * 8 * 2
+
+
+def test_cli_usage_without_gpu():
+    """The Next-Week driver parses its flags before touching a device."""
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(nw.__file__), "bin", "rtmi_nw_render")
+    r = subprocess.run([exe, "--bogus"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "usage" in r.stderr
+    r = subprocess.run([exe, "--scene", "nope"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "unknown scene" in r.stderr

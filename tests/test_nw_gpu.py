@@ -112,3 +112,30 @@ def test_final_scene_statistics_vs_reference_gallery(earth):
     # measured at 1024 spp: bias -0.55, tile MAE 0.59 (before the medium rules of
     # bias -12.7, tile MAE 12.9)
     assert abs(d.mean()) < 1.0 and td.mean() < 1.0 and td.max() < 6
+
+
+def test_cli_matches_library(tmp_path, earth):
+    """bin/rtmi_nw_render (main.cu main() as a driver): its P3 is the library's
+    sums quantised as main.cu:567-575 (unclamped), scene by name or number."""
+    import subprocess
+
+    from PIL import Image
+
+    exe = os.path.join(os.path.dirname(nw.__file__), "bin", "rtmi_nw_render")
+    tex = tmp_path / "earth.ppm"
+    Image.fromarray(earth).save(tex)
+    W, H, spp = 24, 16, 4
+    for scene, which in (("final", 8), ("5", 5)):
+        out = tmp_path / f"o{which}.ppm"
+        subprocess.run([exe, "--scene", scene, "--width", str(W), "--height", str(H), "--spp", str(spp),
+                        "--texture", str(tex), "--out", str(out)], check=True, capture_output=True, timeout=120)
+        tok = out.read_text().split()
+        assert tok[:4] == ["P3", str(W), str(H), "255"]
+        got = np.array(tok[4:], np.int64).reshape(H, W, 3)
+        s, cam = nw.preset(which, image=earth, aspect=W / H)
+        r = nw.NwRenderer(s)
+        sums = r.render(cam, W, H, spp, 50, SEED)
+        r.close()
+        mean = (sums / np.float32(spp)).astype(np.float32)
+        want = np.floor(255.99 * np.sqrt(mean).astype(np.float32).astype(np.float64)).astype(np.int64)[::-1]
+        assert np.array_equal(got, want)

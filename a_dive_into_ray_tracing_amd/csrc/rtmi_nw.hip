@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cstring>
 #include <memory>
+#include <type_traits>
 
 #include "rtmi_internal.h"
 #include "rtmi_nw_internal.h"
@@ -33,19 +34,60 @@ struct Args {
   int32_t tiles_x, tiles, chunk, nch, n_items;
 };
 
-constexpr int kWaves = 4;  // waves per block
+// Two kernel shapes, the same per-path arithmetic (bit-identical images):
+//  * persistent (default when the scene fits in LDS): one 16-wave block per
+//    CU stages the BVH nodes — and the objects, when they fit too — into LDS
+//    once for the whole launch; its waves pull work items from a global
+//    counter, so no wave waits for a slow item of another;
+//  * grid: one wave per work item in 4-wave blocks, nodes in LDS when they
+//    fit the per-block budget (several blocks per CU), else in global memory.
+// Measured (profiles/r01/nw): 4-wave grid blocks beat 8-wave ones (a block's
+// LDS stays allocated until its slowest item ends), LDS nodes +23% and LDS
+// objects +13% on the motion-blur scene.
+#ifndef RTMI_NW_WAVES
+#define RTMI_NW_WAVES 4
+#endif
+#ifndef RTMI_NW_LDS_KB
+#define RTMI_NW_LDS_KB 34
+#endif
+#ifndef RTMI_NW_PERSIST
+#define RTMI_NW_PERSIST 1
+#endif
+#ifndef RTMI_NW_LDS_OBJS
+#define RTMI_NW_LDS_OBJS 1
+#endif
+constexpr int kWaves = RTMI_NW_WAVES;                         // grid kernel: waves per block
+constexpr size_t kLdsBudget = size_t(RTMI_NW_LDS_KB) * 1024;  // grid kernel: staged bytes per block
+constexpr int kPWaves = 16;                                   // persistent kernel: waves per block (one per CU)
+constexpr size_t kPLdsBudget = 136 * 1024;                    // persistent kernel: staged bytes (+ 24 KB accumulators)
 
 __device__ __forceinline__ int64_t fixed(float c) { return int64_t(c * 4294967296.0f); }
 
-template <bool CHUNKED>
-__global__ __launch_bounds__(64 * kWaves) void render_kernel(View sc, Args a, unsigned long long *__restrict__ accum,
-                                                             float *__restrict__ out,
-                                                             unsigned long long *__restrict__ segments) {
-  __shared__ unsigned long long acc[kWaves][3][64];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int item = blockIdx.x * kWaves + wave;
-  if (item >= a.n_items) return;  // wave-uniform
+template <bool LDS_NODES, bool LDS_OBJS>
+__device__ __forceinline__ void stage_scene(const View &sc) {
+  if constexpr (LDS_NODES) {  // BVH nodes (lo[], hi[]), then objects and their insertion indices
+    for (int i = threadIdx.x; i < sc.nnodes; i += blockDim.x) {
+      nw_nodes_lds[i] = sc.nlo[i];
+      nw_nodes_lds[sc.nnodes + i] = sc.nhi[i];
+    }
+    if constexpr (LDS_OBJS) {
+      const float4 *src = reinterpret_cast<const float4 *>(sc.obj);
+      float4 *dst = nw_nodes_lds + 2 * sc.nnodes;
+      for (int i = threadIdx.x; i < 3 * sc.nobj; i += blockDim.x) dst[i] = src[i];
+      int32_t *ids = reinterpret_cast<int32_t *>(dst + 3 * sc.nobj);
+      for (int i = threadIdx.x; i < sc.nobj; i += blockDim.x) ids[i] = sc.obj_id[i];
+    }
+    __syncthreads();
+  }
+}
+
+// One work item = (8x8 tile, <= chunk samples) on one wave: lanes pull
+// (pixel, sample) jobs from the item's queue and regenerate paths as theirs
+// end; sums in the wave's LDS accumulator, then one global add per pixel.
+template <bool CHUNKED, bool LDS_NODES, bool LDS_OBJS>
+__device__ __forceinline__ void run_item(const View &sc, const Args &a, int item, int lane,
+                                         unsigned long long (&acc)[3][64], unsigned long long *__restrict__ accum,
+                                         float *__restrict__ out, unsigned &nseg) {
   const int tile = item / a.nch;
   const int s0 = (item - tile * a.nch) * a.chunk;
   const int ns = min(a.chunk, a.spp - s0);
@@ -55,10 +97,9 @@ __global__ __launch_bounds__(64 * kWaves) void render_kernel(View sc, Args a, un
   const int nv = vw * vh;
   const int nq = nv * ns;
 
-  acc[wave][0][lane] = 0;
-  acc[wave][1][lane] = 0;
-  acc[wave][2][lane] = 0;
-  unsigned nseg = 0;
+  acc[0][lane] = 0;
+  acc[1][lane] = 0;
+  acc[2][lane] = 0;
 
   V o, d, T;
   float time = 0.f;
@@ -94,13 +135,13 @@ __global__ __launch_bounds__(64 * kWaves) void render_kernel(View sc, Args a, un
       const uint64_t seg_key = sc.has_media ? rng.next() : 0ull;
       float t;
       int face;
-      const int32_t k = hit_world_nw(sc, o, d, time, seg_key, t, face);
+      const int32_t k = hit_world_nw<LDS_NODES, LDS_OBJS>(sc, o, d, time, seg_key, t, face);
       if (k < 0) {  // background main.cu:92-99
         col = mk(T.x * sc.bg[0], T.y * sc.bg[1], T.z * sc.bg[2]);
         done = true;
       } else {
-        const Obj ob = k < sc.nobj ? sc.obj[k] : sc.med[k - sc.nobj];
-        const Rec rec = make_rec(sc, ob, o, d, time, t, face);
+        const Rec rec = k < sc.nobj ? make_rec(sc, sc.obj[k], o, d, time, t, face)
+                                    : make_rec_medium(sc, sc.med[k - sc.nobj], o, d, time);
         const Mat m = sc.mat[rec.mat];
         V at, nd;
         if (m.kind == kDiffuseLight) {  // emitted, no scatter: main.cu:76-90
@@ -122,9 +163,9 @@ __global__ __launch_bounds__(64 * kWaves) void render_kernel(View sc, Args a, un
     const unsigned long long m = __ballot(done);
     if (m) {
       if (done) {
-        atomicAdd(&acc[wave][0][px], (unsigned long long)fixed(col.x));
-        atomicAdd(&acc[wave][1][px], (unsigned long long)fixed(col.y));
-        atomicAdd(&acc[wave][2][px], (unsigned long long)fixed(col.z));
+        atomicAdd(&acc[0][px], (unsigned long long)fixed(col.x));
+        atomicAdd(&acc[1][px], (unsigned long long)fixed(col.y));
+        atomicAdd(&acc[2][px], (unsigned long long)fixed(col.z));
         const int rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
         const int q = next + rank;
         if (q < nq) start(q);
@@ -133,21 +174,99 @@ __global__ __launch_bounds__(64 * kWaves) void render_kernel(View sc, Args a, un
       next += __popcll(m);
     }
   }
-  // wave sum of segments (lanes' counts) -> one atomic
-  unsigned long long ws = nseg;
-  for (int off = 32; off > 0; off >>= 1) ws += __shfl_xor(ws, off);
-  if (lane == 0) atomicAdd(segments, ws);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   if (lane < nv) {
     const int ly = lane / vw, lx = lane - ly * vw;
     const size_t o3 = (size_t(y0 + ly) * size_t(a.W) + size_t(x0 + lx)) * 3;
     for (int c = 0; c < 3; ++c) {
-      const unsigned long long v = acc[wave][c][lane];
+      const unsigned long long v = acc[c][lane];
       if constexpr (CHUNKED) atomicAdd(&accum[o3 + c], v);
       else out[o3 + c] = float((long long)v) * 0x1p-32f;
     }
   }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ void add_segments(unsigned nseg, int lane, unsigned long long *segments) {
+  unsigned long long ws = nseg;  // wave sum of the lanes' world.hit calls -> one atomic
+  for (int off = 32; off > 0; off >>= 1) ws += __shfl_xor(ws, off);
+  if (lane == 0) atomicAdd(segments, ws);
+}
+
+template <bool CHUNKED, bool LDS_NODES, bool LDS_OBJS>
+__global__ __launch_bounds__(64 * kWaves) void render_kernel(View sc, Args a, unsigned long long *__restrict__ accum,
+                                                             float *__restrict__ out,
+                                                             unsigned long long *__restrict__ segments) {
+  __shared__ unsigned long long acc[kWaves][3][64];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int item = blockIdx.x * kWaves + wave;
+  stage_scene<LDS_NODES, LDS_OBJS>(sc);  // block barrier inside: before any wave leaves
+  if (item >= a.n_items) return;         // wave-uniform
+  unsigned nseg = 0;
+  run_item<CHUNKED, LDS_NODES, LDS_OBJS>(sc, a, item, lane, acc[wave], accum, out, nseg);
+  add_segments(nseg, lane, segments);
+}
+
+template <bool CHUNKED, bool LDS_OBJS>
+__global__ __launch_bounds__(64 * kPWaves) void render_persistent(View sc, Args a,
+                                                                  unsigned long long *__restrict__ accum,
+                                                                  float *__restrict__ out,
+                                                                  unsigned long long *__restrict__ segments,
+                                                                  unsigned *__restrict__ counter) {
+  __shared__ unsigned long long acc[kPWaves][3][64];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  stage_scene<true, LDS_OBJS>(sc);
+  unsigned nseg = 0;
+  for (;;) {  // every wave leaves when the counter passes n_items
+    unsigned it = 0;
+    if (lane == 0) it = atomicAdd(counter, 1u);
+    it = __builtin_amdgcn_readfirstlane(__shfl(it, 0));
+    if (int(it) >= a.n_items) break;
+    run_item<CHUNKED, true, LDS_OBJS>(sc, a, int(it), lane, acc[wave], accum, out, nseg);
+  }
+  add_segments(nseg, lane, segments);
+}
+
+// Debug (parity investigations): the segments of ONE camera sample (pixel
+// i, j, sample s): per segment o.xyz, d.xyz, t, winner insertion index (as
+// float bits) — the oracle's or_nw_trace records the same.
+__global__ void trace_kernel(View sc, Args a, int i, int j, int s, float *rec, int cap, int *n_out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Xoro rng;
+  rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(s));
+  float ju, jv;
+  rng.pair(ju, jv);
+  V o, d;
+  get_ray<true, float>(a.cam, (float(i) + ju) / float(a.W), (float(j) + jv) / float(a.H), rng, o, d);
+  const float time = __builtin_fmaf(rng.uni(), a.time1 - a.time0, a.time0);
+  int n = 0;
+  for (int depth = 0; depth < a.max_depth && n < cap; ++depth) {
+    const uint64_t seg_key = sc.has_media ? rng.next() : 0ull;
+    float t;
+    int face;
+    const int32_t k = hit_world_nw<false, false>(sc, o, d, time, seg_key, t, face);
+    float *r = rec + 12 * n++;
+    r[0] = o.x; r[1] = o.y; r[2] = o.z; r[3] = d.x; r[4] = d.y; r[5] = d.z; r[6] = t;
+    r[7] = __int_as_float(k < 0 ? -1 : k < sc.nobj ? sc.obj_id[k] : sc.med_id[k - sc.nobj]);
+    r[8] = r[9] = r[10] = 0.f;
+    r[11] = __int_as_float(face);
+    if (k < 0) break;
+    const Rec rc = k < sc.nobj ? make_rec(sc, sc.obj[k], o, d, time, t, face) : make_rec_medium(sc, sc.med[k - sc.nobj], o, d, time);
+    r[8] = rc.n.x; r[9] = rc.n.y; r[10] = rc.n.z;
+#ifdef RTMI_NW_DBG
+    if (k < sc.nobj) { r[8] = float(sc.obj[k].ka & 255); r[9] = float(sc.obj[k].inst); r[10] = float(k); r[11] = float(sc.obj[k].mat); }
+#endif
+    const Mat m = sc.mat[rc.mat];
+    V at, nd;
+    if (m.kind == kDiffuseLight || !scatter_nw(sc, rc, d, rng, at, nd)) break;
+    o = rc.p;
+    d = nd;
+  }
+  *n_out = n;
 }
 
 __global__ void finalize_kernel(const unsigned long long *__restrict__ acc, float *__restrict__ out, size_t n) {
@@ -173,7 +292,7 @@ using namespace rtmi::nw;
 struct rt_nw_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  Obj *obj = nullptr;
+  DevObj *obj = nullptr;
   int32_t *obj_id = nullptr;
   Obj *med = nullptr;
   int32_t *med_id = nullptr;
@@ -185,7 +304,7 @@ struct rt_nw_ctx {
   int32_t *pperm = nullptr;
   uint8_t *img = nullptr;
   Image *imgd = nullptr;
-  Node *nodes = nullptr;
+  float4 *nodes = nullptr;  // 2 * nnodes: lo[] then hi[]
   int32_t nobj = 0, nnodes = 0, ninst = 0, nmat = 0, ntex = 0;
   float bg[3] = {0.f, 0.f, 0.f};
   int32_t has_media = 0;
@@ -194,6 +313,8 @@ struct rt_nw_ctx {
   float *scratch = nullptr;
   size_t scratch_cap = 0;
   unsigned long long *segments = nullptr;
+  unsigned *counter = nullptr;  // persistent kernel's work-item counter
+  int32_t persist_blocks = 0;   // resident 16-wave blocks (CUs x blocks per CU)
 };
 
 namespace {
@@ -243,7 +364,8 @@ View view_of(const rt_nw_ctx *c) {
   v.perlin_perm = c->pperm;
   v.image_px = c->img;
   v.image = c->imgd;
-  v.nodes = c->nodes;
+  v.nlo = c->nodes;
+  v.nhi = c->nodes + c->nnodes;
   v.nnodes = c->nnodes;
   for (int i = 0; i < 3; ++i) v.bg[i] = c->bg[i];
   v.has_media = c->has_media;
@@ -268,6 +390,13 @@ RTMI_EXPORT int rt_nw_ctx_create(int32_t device, rt_nw_ctx **out) {
   HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
   if (int rc = alloc_copy<unsigned long long>(&ctx->segments, nullptr, 1)) return rc;
   HIP_TRY(hipMemset(ctx->segments, 0, sizeof(unsigned long long)));
+  if (int rc = alloc_copy<unsigned>(&ctx->counter, nullptr, 1)) return rc;
+  {
+    int per_cu = 0;  // the persistent grid: what stays resident (VGPR-limited: one 16-wave block per CU)
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<true, false>,
+                                                         64 * kPWaves, 0));
+    ctx->persist_blocks = per_cu * prop.multiProcessorCount;
+  }
   *out = ctx.release();
   return RT_OK;
 }
@@ -278,7 +407,7 @@ RTMI_EXPORT int rt_nw_ctx_destroy(rt_nw_ctx *ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   for (void *p : {(void *)ctx->obj, (void *)ctx->obj_id, (void *)ctx->med, (void *)ctx->med_id, (void *)ctx->inst, (void *)ctx->mat, (void *)ctx->tex,
                   (void *)ctx->pvec, (void *)ctx->pperm, (void *)ctx->img, (void *)ctx->imgd, (void *)ctx->nodes,
-                  (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments})
+                  (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments, (void *)ctx->counter})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -309,12 +438,35 @@ RTMI_EXPORT int rt_nw_ctx_set_scene(rt_nw_ctx *ctx, rt_nw_scene *s) {
     if (t.kind == kNoise && (t.a < 0 || t.a >= np)) return set_error(RT_EINVAL, "rt_nw: bad perlin index");
     if (t.kind == kImage && (t.a < 0 || t.a >= nim)) return set_error(RT_EINVAL, "rt_nw: bad image index");
   }
+  // nodes as lo[] = {bmin, skip} and hi[] = {bmax, leaf} (two independent loads)
+  std::vector<float4> split(2 * ds.nodes.size());
+  for (size_t i = 0; i < ds.nodes.size(); ++i) {
+    const Node &nd = ds.nodes[i];
+    float sk, lf;
+    std::memcpy(&sk, &nd.skip, 4);
+    std::memcpy(&lf, &nd.leaf, 4);
+    split[i] = make_float4(nd.bmin[0], nd.bmin[1], nd.bmin[2], sk);
+    split[ds.nodes.size() + i] = make_float4(nd.bmax[0], nd.bmax[1], nd.bmax[2], lf);
+  }
+  std::vector<DevObj> dobj(ds.obj.size());
+  for (size_t i = 0; i < ds.obj.size(); ++i) {
+    const Obj &o = ds.obj[i];
+    DevObj &q = dobj[i];
+    for (int c = 0; c < 4; ++c) {
+      q.g0[c] = o.g0[c];
+      q.g1[c] = o.g1[c];
+    }
+    q.ka = o.kind | (o.aux << 8);
+    q.mat = o.mat;
+    q.t1 = o.g2[0];
+    q.inst = o.inst;
+  }
   std::vector<float4> pv(ds.perlin_vec.size() / 4);
   std::memcpy(pv.data(), ds.perlin_vec.data(), pv.size() * sizeof(float4));
   Guard g(ctx->device);
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   int rc;
-  if ((rc = alloc_copy(&ctx->obj, ds.obj.data(), ds.obj.size())) ||
+  if ((rc = alloc_copy(&ctx->obj, dobj.data(), dobj.size())) ||
       (rc = alloc_copy(&ctx->med, ds.med.data(), ds.med.size())) ||
       (rc = alloc_copy(&ctx->med_id, ds.med_id.data(), ds.med_id.size())) ||
       (rc = alloc_copy(&ctx->obj_id, ds.obj_id.data(), ds.obj_id.size())) ||
@@ -324,7 +476,7 @@ RTMI_EXPORT int rt_nw_ctx_set_scene(rt_nw_ctx *ctx, rt_nw_scene *s) {
       (rc = alloc_copy(&ctx->pperm, ds.perlin_perm.data(), ds.perlin_perm.size())) ||
       (rc = alloc_copy(&ctx->img, ds.image_px.data(), ds.image_px.size())) ||
       (rc = alloc_copy(&ctx->imgd, ds.image.data(), ds.image.size())) ||
-      (rc = alloc_copy(&ctx->nodes, ds.nodes.data(), ds.nodes.size())))
+      (rc = alloc_copy(&ctx->nodes, split.data(), split.size())))
     return rc;
   ctx->nobj = int32_t(ds.obj.size());
   ctx->nmed = int32_t(ds.med.size());
@@ -378,8 +530,31 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
   if (valid < nrows)  // rows past H: zero
     HIP_TRY(hipMemsetAsync(dev_strip + size_t(valid) * W * 3, 0, size_t(nrows - valid) * W * 3 * sizeof(float), st));
   HIP_TRY(hipMemsetAsync(ctx->segments, 0, sizeof(unsigned long long), st));
-  const unsigned blocks = unsigned((a.n_items + kWaves - 1) / kWaves);
   const View v = view_of(ctx);
+  const size_t node_bytes = size_t(ctx->nnodes) * 32, obj_bytes = size_t(ctx->nobj) * (sizeof(DevObj) + 4);
+  // persistent: everything that fits one CU's LDS budget; else the grid kernel
+  const bool persist = RTMI_NW_PERSIST && ctx->nnodes > 0 && node_bytes <= kPLdsBudget && ctx->persist_blocks > 0;
+  const bool p_objs = RTMI_NW_LDS_OBJS && persist && node_bytes + obj_bytes <= kPLdsBudget;
+  const bool lds_nodes = !persist && ctx->nnodes > 0 && node_bytes <= kLdsBudget,
+             lds_objs = RTMI_NW_LDS_OBJS && lds_nodes && node_bytes + obj_bytes <= kLdsBudget;
+  const size_t lds = persist ? (p_objs ? node_bytes + obj_bytes : node_bytes)
+                             : lds_objs ? node_bytes + obj_bytes : lds_nodes ? node_bytes : 0;
+  const unsigned blocks = persist ? unsigned(std::min<int64_t>(ctx->persist_blocks, (a.n_items + kPWaves - 1) / kPWaves))
+                                  : unsigned((a.n_items + kWaves - 1) / kWaves);
+  if (persist) HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
+  auto launch = [&](auto chunked) {
+    constexpr bool C = decltype(chunked)::value;
+    if (persist && p_objs)
+      hipLaunchKernelGGL((render_persistent<C, true>), dim3(blocks), dim3(64 * kPWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments, ctx->counter);
+    else if (persist)
+      hipLaunchKernelGGL((render_persistent<C, false>), dim3(blocks), dim3(64 * kPWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments, ctx->counter);
+    else if (lds_objs)
+      hipLaunchKernelGGL((render_kernel<C, true, true>), dim3(blocks), dim3(64 * kWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments);
+    else if (lds_nodes)
+      hipLaunchKernelGGL((render_kernel<C, true, false>), dim3(blocks), dim3(64 * kWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments);
+    else
+      hipLaunchKernelGGL((render_kernel<C, false, false>), dim3(blocks), dim3(64 * kWaves), 0, st, v, a, ctx->accum, dev_strip, ctx->segments);
+  };
   if (a.nch > 1) {
     const size_t nv = size_t(valid) * W * 3;
     if (nv > ctx->accum_cap) {
@@ -388,13 +563,11 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
       ctx->accum_cap = nv;
     }
     HIP_TRY(hipMemsetAsync(ctx->accum, 0, nv * sizeof(unsigned long long), st));
-    hipLaunchKernelGGL(render_kernel<true>, dim3(blocks), dim3(64 * kWaves), 0, st, v, a, ctx->accum, dev_strip,
-                       ctx->segments);
+    launch(std::true_type{});
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(finalize_kernel, dim3(unsigned((nv + 255) / 256)), dim3(256), 0, st, ctx->accum, dev_strip, nv);
   } else {
-    hipLaunchKernelGGL(render_kernel<false>, dim3(blocks), dim3(64 * kWaves), 0, st, v, a, ctx->accum, dev_strip,
-                       ctx->segments);
+    launch(std::false_type{});
   }
   HIP_TRY(hipGetLastError());
   return RT_OK;
@@ -414,6 +587,33 @@ RTMI_EXPORT int rt_nw_render(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32_t W,
   if (int rc = rt_nw_render_rows(ctx, cam, W, H, spp, max_depth, seed, 0, 1, H, ctx->scratch, ctx->stream)) return rc;
   HIP_TRY(hipMemcpyAsync(sum, ctx->scratch, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_nw_debug_trace(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32_t W, int32_t H, int32_t max_depth,
+                                  uint64_t seed, int32_t i, int32_t j, int32_t s, float *rec, int32_t cap, int32_t *n) {
+  if (!ctx || !cam || !rec || !n || cap < 1 || max_depth < 1 || i < 0 || i >= W || j < 0 || j >= H)
+    return set_error(RT_EINVAL, "rt_nw_debug_trace: bad argument");
+  Guard g(ctx->device);
+  Args a{};
+  a.cam = camf(cam->cam);
+  a.time0 = float(cam->time0);
+  a.time1 = float(cam->time1);
+  a.W = W;
+  a.H = H;
+  a.max_depth = max_depth;
+  a.seed = seed;
+  float *d_rec = nullptr;
+  int *d_n = nullptr;
+  HIP_TRY(hipMalloc(&d_rec, size_t(cap) * 12 * sizeof(float)));
+  HIP_TRY(hipMalloc(&d_n, sizeof(int)));
+  hipLaunchKernelGGL(trace_kernel, dim3(1), dim3(64), 0, ctx->stream, view_of(ctx), a, i, j, s, d_rec, cap, d_n);
+  hipError_t e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) e = hipMemcpy(n, d_n, sizeof(int), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(rec, d_rec, size_t(*n) * 12 * sizeof(float), hipMemcpyDeviceToHost);
+  (void)hipFree(d_rec);
+  (void)hipFree(d_n);
+  if (e != hipSuccess) return set_error(RT_EHIP, "rt_nw_debug_trace: %s", hipGetErrorString(e));
   return RT_OK;
 }
 

@@ -104,7 +104,7 @@ __device__ __forceinline__ float nw_acosf(float x) {
 // scene view
 // ---------------------------------------------------------------------------
 struct View {
-  const Obj *obj;  // non-media objects, BVH leaf order
+  const DevObj *obj;  // non-media objects, BVH leaf order
   const int32_t *obj_id;
   const Obj *med;  // media, insertion order (evaluated before the BVH walk)
   const int32_t *med_id;
@@ -116,7 +116,7 @@ struct View {
   const int32_t *perlin_perm;
   const uint8_t *image_px;
   const Image *image;
-  const Node *nodes;
+  const float4 *nlo, *nhi;  // BVH nodes split into {bmin, skip} and {bmax, leaf} (global memory)
   int32_t nnodes;
   float bg[3];
   int32_t has_media;
@@ -159,8 +159,12 @@ __device__ __forceinline__ bool hit_sphere(V o, V d, V c, float r, float tmin, f
   return false;
 }
 // moving_sphere::center moving_sphere.h:44-46
-__device__ __forceinline__ V moving_center(const Obj &ob, float time) {
-  const float f = (time - ob.g1[3]) / (ob.g2[0] - ob.g1[3]);
+__device__ __forceinline__ float time1_of(const Obj &ob) { return ob.g2[0]; }
+__device__ __forceinline__ float time1_of(const DevObj &ob) { return ob.t1; }
+template <class O> __device__ __forceinline__ V moving_center(const O &ob, float time) {
+  // over [0, 1] (every reference scene) the quotient is exactly `time`: skip the division
+  const float t1 = time1_of(ob);
+  const float f = (ob.g1[3] == 0.0f && t1 == 1.0f) ? time : (time - ob.g1[3]) / (t1 - ob.g1[3]);
   return mk(__builtin_fmaf(f, ob.g1[0] - ob.g0[0], ob.g0[0]), __builtin_fmaf(f, ob.g1[1] - ob.g0[1], ob.g0[1]),
             __builtin_fmaf(f, ob.g1[2] - ob.g0[2], ob.g0[2]));
 }
@@ -263,16 +267,17 @@ __device__ __forceinline__ float medium_uniform(uint64_t seg_key, int32_t id, in
 
 // One non-medium object's hit (world ray in; t_min = 0.001, no upper bound:
 // the caller applies the order-independent closest rule).  face: box side.
-__device__ __forceinline__ bool hit_object(const View &sc, const Obj &ob, V ow, V dw, float time, float &t,
+__device__ __forceinline__ bool hit_object(const View &sc, const DevObj &ob, V ow, V dw, float time, float &t,
                                            int &face) {
   V o = ow, d = dw;
   if (ob.inst >= 0) to_local(sc.inst[ob.inst], o, d);
   const float tmin = 0.001f;
-  switch (ob.kind) {
+  const int kind = ob.ka & 255;
+  switch (kind) {
     case kSphere: return hit_sphere(o, d, mk(ob.g0[0], ob.g0[1], ob.g0[2]), ob.g0[3], tmin, INFINITY, t);
     case kMovingSphere: return hit_moving(o, d, moving_center(ob, time), ob.g0[3], tmin, INFINITY, t);
     case kRectXY: case kRectXZ: case kRectYZ:
-      return hit_rect_kind(ob.kind, o, d, ld4(ob.g0), ob.g1[0], tmin, INFINITY, t);
+      return hit_rect_kind(kind, o, d, ld4(ob.g0), ob.g1[0], tmin, INFINITY, t);
     default: face = hit_box(o, d, ld4(ob.g0), ld4(ob.g1), tmin, INFINITY, t); return face >= 0;
   }
 }
@@ -284,8 +289,19 @@ __device__ __forceinline__ bool hit_object(const View &sc, const Obj &ob, V ow, 
 // the smallest (t, insertion index) pair, so no result depends on the visit
 // order.  Returns the winner's index: [0, nobj) an object in leaf order,
 // nobj + m medium m; -1 none.
+// The BVH nodes live in LDS when they fit (staged per block by the kernel,
+// rtmi_nw.hip), otherwise in global memory: the walk is a chain of dependent
+// node loads.
+// LDS layout (dynamic shared memory): nodes lo[nnodes], hi[nnodes]; then, when
+// they fit too, the objects (4 float4 each) and their insertion indices.
+extern __shared__ float4 nw_nodes_lds[];
+template <bool LDS_NODES, bool LDS_OBJS>
 __device__ __forceinline__ int32_t hit_world_nw(const View &sc, V o, V d, float time, uint64_t seg_key, float &best_t,
                                                 int &best_face) {
+  const float4 *nlo = LDS_NODES ? nw_nodes_lds : sc.nlo;
+  const float4 *nhi = LDS_NODES ? nw_nodes_lds + sc.nnodes : sc.nhi;
+  const DevObj *objs = LDS_OBJS ? reinterpret_cast<const DevObj *>(nw_nodes_lds + 2 * sc.nnodes) : sc.obj;
+  const int32_t *oids = LDS_OBJS ? reinterpret_cast<const int32_t *>(nw_nodes_lds + 2 * sc.nnodes + 3 * sc.nobj) : sc.obj_id;
   best_t = INFINITY;
   int32_t best = -1, best_id = 0x7fffffff;
   best_face = -1;
@@ -310,21 +326,23 @@ __device__ __forceinline__ int32_t hit_world_nw(const View &sc, V o, V d, float 
   const float ox = -o.x * ix, oy = -o.y * iy, oz = -o.z * iz;
   int32_t node = 0;
   while (node < sc.nnodes) {
-    const Node nd = sc.nodes[node];
-    const float tx0 = __builtin_fmaf(nd.bmin[0], ix, ox), tx1 = __builtin_fmaf(nd.bmax[0], ix, ox);
-    const float ty0 = __builtin_fmaf(nd.bmin[1], iy, oy), ty1 = __builtin_fmaf(nd.bmax[1], iy, oy);
-    const float tz0 = __builtin_fmaf(nd.bmin[2], iz, oz), tz1 = __builtin_fmaf(nd.bmax[2], iz, oz);
+    const float4 lo = nlo[node], hi = nhi[node];
+    const float tx0 = __builtin_fmaf(lo.x, ix, ox), tx1 = __builtin_fmaf(hi.x, ix, ox);
+    const float ty0 = __builtin_fmaf(lo.y, iy, oy), ty1 = __builtin_fmaf(hi.y, iy, oy);
+    const float tz0 = __builtin_fmaf(lo.z, iz, oz), tz1 = __builtin_fmaf(hi.z, iz, oz);
     const float tnear = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx0, tx1), __builtin_fminf(ty0, ty1)),
                                         __builtin_fmaxf(__builtin_fminf(tz0, tz1), 0.0f));
     const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx0, tx1), __builtin_fmaxf(ty0, ty1)),
                                        __builtin_fminf(__builtin_fmaxf(tz0, tz1), best_t));
     const bool enter = tnear <= tfar;
-    if (enter && nd.leaf >= 0) {
-      const int32_t first = nd.leaf >> 4, cnt = nd.leaf & 15;
+    const int32_t leaf = __float_as_int(hi.w);
+    if (enter && leaf >= 0) {
+      const int32_t first = leaf >> 4, cnt = leaf & 15;
       for (int32_t k = first; k < first + cnt; ++k) {
-        const Obj ob = sc.obj[k];
-        if (ob.aux > 0 && ((med_hit >> (ob.aux - 1)) & 1u)) continue;  // hidden by its medium
-        const int32_t id = sc.obj_id[k];
+        const DevObj ob = objs[k];
+        const int twin = ob.ka >> 8;
+        if (twin > 0 && ((med_hit >> (twin - 1)) & 1u)) continue;  // hidden by its medium
+        const int32_t id = oids[k];
         float t;
         int face = -1;
         if (hit_object(sc, ob, o, d, time, t, face) && (t < best_t || (t == best_t && id < best_id))) {
@@ -335,7 +353,7 @@ __device__ __forceinline__ int32_t hit_world_nw(const View &sc, V o, V d, float 
         }
       }
     }
-    node = enter ? node + 1 : nd.skip;
+    node = enter ? node + 1 : __float_as_int(lo.w);
   }
   return best;
 }
@@ -431,22 +449,26 @@ struct Rec {
   float u, v;
   int32_t mat;
 };
-__device__ __forceinline__ Rec make_rec(const View &sc, const Obj &ob, V ow, V dw, float time, float t, int face) {
+// constant_medium.h:73-77: p at the entry point, arbitrary normal
+__device__ __forceinline__ Rec make_rec_medium(const View &sc, const Obj &ob, V ow, V dw, float time) {
   Rec r;
   r.mat = ob.mat;
   r.u = 0.0f;
   r.v = 0.0f;
-  if (ob.kind == kMedium) {  // constant_medium.h:73-77: p at the entry point, arbitrary normal
-    V o = ow, d = dw;
-    const Inst in = ob.inst >= 0 ? sc.inst[ob.inst] : Inst{1.f, 0.f, {0.f, 0.f, 0.f}, 0, {0, 0}};
-    if (ob.inst >= 0) to_local(in, o, d);
-    float r1;
-    (void)hit_boundary(ob, o, d, time, -INFINITY, INFINITY, r1);
-    if (r1 < 0.0f) r1 = 0.0f;
-    r.p = at3(ow, dw, r1);
-    r.n = mk(1.0f, 0.0f, 0.0f);
-    return r;
-  }
+  V o = ow, d = dw;
+  if (ob.inst >= 0) to_local(sc.inst[ob.inst], o, d);
+  float r1;
+  (void)hit_boundary(ob, o, d, time, -INFINITY, INFINITY, r1);
+  if (r1 < 0.0f) r1 = 0.0f;
+  r.p = at3(ow, dw, r1);
+  r.n = mk(1.0f, 0.0f, 0.0f);
+  return r;
+}
+__device__ __forceinline__ Rec make_rec(const View &sc, const DevObj &ob, V ow, V dw, float time, float t, int face) {
+  Rec r;
+  r.mat = ob.mat;
+  r.u = 0.0f;
+  r.v = 0.0f;
   V o = ow, d = dw;
   Inst in{1.f, 0.f, {0.f, 0.f, 0.f}, 0, {0, 0}};
   if (ob.inst >= 0) {
@@ -456,13 +478,14 @@ __device__ __forceinline__ Rec make_rec(const View &sc, const Obj &ob, V ow, V d
   V p = at3(o, d, t), n;
   const Mat mm = sc.mat[ob.mat];
   const bool need_uv = mm.kind != kDielectric && tex_needs_uv(sc, mm.tex);
-  if (ob.kind == kSphere || ob.kind == kMovingSphere) {
-    const V c = ob.kind == kSphere ? mk(ob.g0[0], ob.g0[1], ob.g0[2]) : moving_center(ob, time);
+  const int okind = ob.ka & 255;
+  if (okind == kSphere || okind == kMovingSphere) {
+    const V c = okind == kSphere ? mk(ob.g0[0], ob.g0[1], ob.g0[2]) : moving_center(ob, time);
     const float inv_r = 1.0f / ob.g0[3];
     n = mk(inv_r * (p.x - c.x), inv_r * (p.y - c.y), inv_r * (p.z - c.z));
     if (need_uv) sphere_uv(n, r.u, r.v);
   } else {
-    int kind = ob.kind;
+    int kind = okind;
     float a0, a1, b0, b1;
     if (kind == kBox) {  // box face -> its rect (box.h:37-48)
       const float4 p0 = ld4(ob.g0), p1 = ld4(ob.g1);

@@ -340,49 +340,92 @@ int flatten(rt_nw_scene *s) {
   return RT_OK;
 }
 
-// BVH over the flattened objects: median split on the longest centroid axis,
-// leaves of <= kNodeLeafMax objects, DFS order with skip links.  Boxes are
-// the objects' double bounds grown by 1e-3 of the scene scale and rounded
-// outward to float (the RTIOW BVH's margin argument).
+// BVH over the flattened objects, built with the surface-area heuristic
+// (full sweep over the centroid order on each axis): a child's expected cost
+// is its area times the summed test cost of its objects, so a huge object
+// (the R=1000 ground sphere) ends up alone near the root instead of inflating
+// every box on its path, as a median split leaves it.  Leaves of <=
+// kNodeLeafMax objects, DFS order with skip links.  Boxes are the objects'
+// double bounds grown by 1e-3 of the scene scale and rounded outward to float
+// (the RTIOW BVH's margin argument).
 struct ObjBvh {
   const std::vector<Bounds> &b;
+  const std::vector<double> &w;  // per-object test cost (relative)
   double margin;
   std::vector<Node> nodes;
   std::vector<int32_t> order;
 
+  static double area(const double lo[3], const double hi[3]) {
+    const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+  }
   void build(int32_t *ids, int cnt) {
     const int me = int(nodes.size());
     nodes.push_back(Node{});
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int i = 0; i < cnt; ++i)
+    double wsum = 0;
+    for (int i = 0; i < cnt; ++i) {
+      wsum += w[ids[i]];
       for (int a = 0; a < 3; ++a) {
         lo[a] = std::min(lo[a], b[ids[i]].lo[a]);
         hi[a] = std::max(hi[a], b[ids[i]].hi[a]);
-        const double c = 0.5 * (b[ids[i]].lo[a] + b[ids[i]].hi[a]);
-        clo[a] = std::min(clo[a], c);
-        chi[a] = std::max(chi[a], c);
       }
+    }
     Node nd{};
     for (int a = 0; a < 3; ++a) {
       nd.bmin[a] = std::nextafter(float(lo[a] - margin), -INFINITY);
       nd.bmax[a] = std::nextafter(float(hi[a] + margin), INFINITY);
     }
-    if (cnt <= kNodeLeafMax) {
+    // best SAH split: cost = C_trav * A + A_L * W_L + A_R * W_R (A = area)
+    const double pa = std::max(area(lo, hi), 1e-30);
+    double best = INFINITY;
+    int best_ax = -1, best_i = -1;
+    std::vector<double> right_cost(cnt);
+    for (int ax = 0; ax < 3 && cnt > 1; ++ax) {
+      std::sort(ids, ids + cnt, [&](int32_t x, int32_t y) {
+        const double cx = b[x].lo[ax] + b[x].hi[ax], cy = b[y].lo[ax] + b[y].hi[ax];
+        return cx < cy || (cx == cy && x < y);
+      });
+      double rl[3] = {INFINITY, INFINITY, INFINITY}, rh[3] = {-INFINITY, -INFINITY, -INFINITY}, rw = 0;
+      for (int i = cnt - 1; i > 0; --i) {  // right part = ids[i..cnt)
+        rw += w[ids[i]];
+        for (int a = 0; a < 3; ++a) {
+          rl[a] = std::min(rl[a], b[ids[i]].lo[a]);
+          rh[a] = std::max(rh[a], b[ids[i]].hi[a]);
+        }
+        right_cost[i] = area(rl, rh) * rw;
+      }
+      double ll[3] = {INFINITY, INFINITY, INFINITY}, lh[3] = {-INFINITY, -INFINITY, -INFINITY}, lw = 0;
+      for (int i = 1; i < cnt; ++i) {  // left part = ids[0..i)
+        lw += w[ids[i - 1]];
+        for (int a = 0; a < 3; ++a) {
+          ll[a] = std::min(ll[a], b[ids[i - 1]].lo[a]);
+          lh[a] = std::max(lh[a], b[ids[i - 1]].hi[a]);
+        }
+        const double c = area(ll, lh) * lw + right_cost[i];
+        if (c < best) {
+          best = c;
+          best_ax = ax;
+          best_i = i;
+        }
+      }
+    }
+#ifndef RTMI_NW_KTRAV
+#define RTMI_NW_KTRAV 2.0
+#endif
+    const double kTrav = RTMI_NW_KTRAV;  // a node visit against one sphere test
+    const bool leaf = cnt == 1 || (cnt <= kNodeLeafMax && pa * wsum <= kTrav * pa + best);
+    if (leaf) {
       nd.leaf = (int32_t(order.size()) << 4) | cnt;
       for (int i = 0; i < cnt; ++i) order.push_back(ids[i]);
       nd.skip = me + 1;
     } else {
-      int ax = 0;
-      for (int a = 1; a < 3; ++a)
-        if (chi[a] - clo[a] > chi[ax] - clo[ax]) ax = a;
-      const int mid = cnt / 2;
-      std::nth_element(ids, ids + mid, ids + cnt, [&](int32_t x, int32_t y) {
-        const double cx = b[x].lo[ax] + b[x].hi[ax], cy = b[y].lo[ax] + b[y].hi[ax];
+      std::sort(ids, ids + cnt, [&](int32_t x, int32_t y) {
+        const double cx = b[x].lo[best_ax] + b[x].hi[best_ax], cy = b[y].lo[best_ax] + b[y].hi[best_ax];
         return cx < cy || (cx == cy && x < y);
       });
-      build(ids, mid);
-      build(ids + mid, cnt - mid);
+      build(ids, best_i);
+      build(ids + best_i, cnt - best_i);
       nd.leaf = -1;
       nd.skip = int(nodes.size());
     }
@@ -423,7 +466,14 @@ int build_device_scene(rt_nw_scene *s, DeviceScene &out) {
       scale = std::max(scale, std::max(std::fabs(b.lo[a]), std::fabs(b.hi[a])));
     }
   }
-  ObjBvh bvh{s->flat_bounds, 1e-3 * (1.0 + scale), {}, {}};
+  // relative test costs: a box is six rectangle tests, an instance adds a
+  // ray transform
+  std::vector<double> cost(n_all, 1.0);
+  for (int k = 0; k < n_all; ++k) {
+    const Obj &o = s->flat_obj[k];
+    cost[k] = (o.kind == kBox ? 3.0 : o.kind == kMovingSphere ? 1.2 : 1.0) + (o.inst >= 0 ? 0.3 : 0.0);
+  }
+  ObjBvh bvh{s->flat_bounds, cost, 1e-3 * (1.0 + scale), {}, {}};
   const int n = int(ids.size());
   if (n > 0) bvh.build(ids.data(), n);
   out.nodes = std::move(bvh.nodes);

@@ -30,7 +30,18 @@ struct Obj {  // 64 B
   int32_t kind, mat, inst, aux;  // aux: medium -> boundary kind | samples << 8; other objects -> twin
                                  // medium + 1 (0: none): the medium whose boundary this object is
 };
-constexpr int kMaxMedia = 32;  // media are evaluated per segment before the BVH walk (a bit mask)
+constexpr int kMaxMedia = 32;
+// The device's record of a non-medium object (48 B: three float4 loads, 25%
+// less LDS than Obj): media live in their own list, so only the moving
+// sphere's time1 remains of g2.
+struct DevObj {
+  float g0[4], g1[4];
+  int32_t ka;  // kind | aux << 8 (one 32-bit field: no sub-dword loads)
+  int32_t mat;
+  float t1;  // moving sphere: time1 (Obj g2[0])
+  int32_t inst;
+};
+static_assert(sizeof(DevObj) == 48, "DevObj layout");
 struct Inst {  // 32 B; world = translate(rotate_y(local)) (hittable.h:49-189)
   float c, s;      // cos, sin of the composed rotate_y angle
   float off[3];    // composed translation

@@ -215,6 +215,15 @@ class NwRenderer:
         check(load().rt_nw_render_rows(self._h, C.byref(cam), W, H, spp, max_depth, seed, row0, row_step, nrows,
                                        C.c_void_p(dev_ptr), C.c_void_p(stream)), "rt_nw_render_rows")
 
+    def debug_trace(self, cam, W, H, i, j, s, max_depth=50, seed=1984, cap=64):
+        """The segments of one camera sample: rows (o.xyz, d.xyz, t, n.xyz) and (winner index, box face)."""
+        rec = np.zeros(12 * cap, np.float32)
+        n = C.c_int32()
+        check(load().rt_nw_debug_trace(self._h, C.byref(cam), W, H, max_depth, seed, i, j, s, rec.ctypes.data_as(_fp), cap,
+                                       C.byref(n)), "rt_nw_debug_trace")
+        out = rec[: 12 * n.value].reshape(-1, 12).copy()
+        return out[:, [0, 1, 2, 3, 4, 5, 6, 8, 9, 10]], out[:, [7, 11]].view(np.int32)
+
     def last_segments(self):
         v = C.c_uint64()
         check(load().rt_nw_ctx_last_segments(self._h, C.byref(v)), "rt_nw_ctx_last_segments")

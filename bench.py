@@ -350,6 +350,7 @@ def bench_nw(args):
             "roofline": None,
             "kernel_ms": round(kernel_ms, 3),
             "segments_per_sample_rank0": round(segs / (nrows * Wn * spp), 4),
+            "objects_bvh_nodes": list(r.info()),
             "vs_baseline_ref": "reference rt_next_week CUDA, random_scene with moving spheres 1200x800x500 in 37.88 s "
                                "(RTX 2060 Max-Q): 12.67 Msamples/s",
         }

@@ -146,6 +146,12 @@ int rt_nw_render(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32_t W, int32_t H, 
 int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32_t W, int32_t H, int32_t spp,
                       int32_t max_depth, uint64_t seed, int32_t row0, int32_t row_step, int32_t nrows,
                       float *dev_strip, void *stream);
+/* Debug (parity investigations): the path segments of ONE camera sample
+ * (pixel i, j, sample s), up to cap: per segment 12 floats o.xyz, d.xyz, t,
+ * the winner's insertion index (int32 bits, -1: miss), its hit-record normal
+ * xyz and the box face (int32 bits, -1: none).  *n = segments. */
+int rt_nw_debug_trace(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32_t W, int32_t H, int32_t max_depth,
+                      uint64_t seed, int32_t i, int32_t j, int32_t s, float *rec, int32_t cap, int32_t *n);
 /* world.hit calls of the last render (waits for it). */
 int rt_nw_ctx_last_segments(rt_nw_ctx *ctx, uint64_t *segments);
 

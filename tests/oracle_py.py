@@ -247,3 +247,19 @@ def nw_math(fn, x):
     out = np.zeros(n, np.float32)
     L.or_nw_math(fn, n, x.ctypes.data_as(_fp), out.ctypes.data_as(_fp))
     return out
+
+
+def nw_trace(flat, nwcam, W, H, depth, seed, i, j, smp, cap=64):
+    """Oracle mirror of NwRenderer.debug_trace."""
+    L = _nw_bind()
+    L.or_nw_trace.argtypes = [C.POINTER(OrNwScene), C.POINTER(OrCamera), C.c_double, C.c_double] + [C.c_int32] * 3 + [
+        C.c_uint64] + [C.c_int32] * 3 + [_fp, C.c_int32]
+    L.or_nw_trace.restype = C.c_int32
+    s = nw_scene(flat)
+    cam = OrCamera()
+    C.memmove(C.byref(cam), C.byref(nwcam.cam), C.sizeof(cam))
+    rec = np.zeros(12 * cap, np.float32)
+    n = L.or_nw_trace(C.byref(s), C.byref(cam), nwcam.time0, nwcam.time1, W, H, depth, seed, i, j, smp,
+                      rec.ctypes.data_as(_fp), cap)
+    out = rec[: 12 * n].reshape(-1, 12).copy()
+    return out[:, [0, 1, 2, 3, 4, 5, 6, 8, 9, 10]], out[:, [7, 11]].view(np.int32)

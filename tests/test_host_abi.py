@@ -17,7 +17,8 @@ GOLD = O.GOLDEN
 
 
 def declared_symbols():
-    hdr = open(os.path.join(REPO, "include", "rtmi.h")).read()
+    inc = os.path.join(REPO, "include")
+    hdr = "".join(open(os.path.join(inc, f)).read() for f in sorted(os.listdir(inc)) if f.endswith(".h"))
     hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
     return sorted(set(re.findall(r"\b(rt_[a-z_]+)\s*\(", hdr)))
 
@@ -28,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     assert len(syms) >= 17
     for s in syms:
         assert hasattr(L, s), s
-    assert set(syms) == set(_abi.SIGNATURES), "ctypes signatures out of sync with include/rtmi.h"
+    assert set(syms) == set(_abi.SIGNATURES), "ctypes signatures out of sync with include/*.h"
 
 
 def test_version():

@@ -130,13 +130,19 @@ constexpr int kPairGroup = RTMI_PAIR_GROUP;  // sphere pairs per scalar-load gro
 __device__ __forceinline__ int64_t to_fixed(float c) { return int64_t(c * 4294967296.0f); }
 __device__ __forceinline__ float from_fixed(int64_t v) { return float(v) * 0x1p-32f; }
 
-// Grid-kernel block shape.  The BVH kernel is latency-bound on its chain of
-// LDS node loads: 8-wave blocks (one staged BVH per 8 waves) at 8 waves per
-// SIMD (64 VGPRs, a few spilled) run config 2 in 52.9 ms against 54.4 with
-// 4-wave blocks at 6 waves per SIMD (LDS-limited); the brute-force loop does
-// not gain (115.4 vs 114.4 ms) and keeps 4-wave blocks.
+// Grid-kernel block shape.  A block holds its wave slots (and LDS) until its
+// slowest wave ends, so big blocks fragment the CU: with 8-wave blocks the
+// per-wave trace shows ~6 500 of 8 192 wave slots resident in steady state.
+// The BVH kernel runs 4-wave blocks at 8 waves per SIMD (64 VGPRs, a few
+// spilled): 16-byte nodes and 16-bit leaf indices keep a block's LDS (BVH +
+// accumulators) under 20 KB, so 8 blocks fit a CU.  Config 2: 16-wave blocks
+// 55.2 ms, 8-wave 52.4, 4-wave (7 per CU, int32 indices) 51.9.  The
+// brute-force loop keeps its own shape (kWavesPerBlock).
+#ifndef RTMI_BVH_WAVES
+#define RTMI_BVH_WAVES 4
+#endif
 template <bool BVH> struct GridShape {
-  static constexpr int waves = BVH ? 8 : kWavesPerBlock;
+  static constexpr int waves = BVH ? RTMI_BVH_WAVES : kWavesPerBlock;
   static constexpr int per_eu = BVH ? 8 : RTMI_WAVES_PER_EU;
 };
 template <int TW, bool CHUNKED, bool BVH>
@@ -180,7 +186,7 @@ __global__ __launch_bounds__(64 * GridShape<BVH>::waves, GridShape<BVH>::per_eu)
   RTMI_TRACE_BEGIN
 #if RTMI_STATS
   unsigned stats[4] = {0, 0, 0, 0};  // groups, groups with a candidate (wave), resolves (lane), sphere resolves (wave)
-  unsigned bvh_stats[2] = {0, 0};    // BVH: node visits, leaf sphere tests (lane)
+  unsigned bvh_stats[5] = {0, 0, 0, 0, 0};  // BVH: node visits, leaf sphere tests (lane); node iterations, leaf-sphere iterations, root resolutions (wave)
 #endif
 
   const SceneView<float> sc{geom, sh0, sh1, a.n};
@@ -291,10 +297,17 @@ __global__ __launch_bounds__(64 * GridShape<BVH>::waves, GridShape<BVH>::per_eu)
     if (a.tile_cost) atomicAdd(&a.tile_cost[tile], unsigned(wave_segs[wave]));
   }
 #if RTMI_STATS
+  // brute force: [1] groups, [2] groups with a candidate, [4] sphere
+  // resolves (wave); BVH: [1] node iterations, [2] leaf-sphere iterations,
+  // [4] root resolutions (wave).  [3] resolves (lane), [5] node visits,
+  // [6] leaf sphere tests (lane).
   if (lane == 0) { atomicAdd(&segments[1], (unsigned long long)stats[0]); atomicAdd(&segments[2], (unsigned long long)stats[1]); atomicAdd(&segments[4], (unsigned long long)stats[3]); }
   atomicAdd(&segments[3], (unsigned long long)stats[2]);
   atomicAdd(&segments[5], (unsigned long long)bvh_stats[0]);
   atomicAdd(&segments[6], (unsigned long long)bvh_stats[1]);
+  atomicAdd(&segments[1], (unsigned long long)bvh_stats[2]);
+  atomicAdd(&segments[2], (unsigned long long)bvh_stats[3]);
+  atomicAdd(&segments[4], (unsigned long long)bvh_stats[4]);
 #endif
   RTMI_TRACE_END(1)
   if (lane < nv) {
@@ -377,7 +390,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
   RTMI_TRACE_BEGIN
 #if RTMI_STATS
   unsigned stats[4] = {0, 0, 0, 0};
-  unsigned bvh_stats[2] = {0, 0};
+  unsigned bvh_stats[5] = {0, 0, 0, 0, 0};
 #endif
   const SceneView<float> sc{geom, sh0, sh1, a.n};
 
@@ -590,10 +603,17 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
   __builtin_amdgcn_wave_barrier();
   if (lane == 0) atomicAdd(segments, wave_segs[wave]);
 #if RTMI_STATS
+  // brute force: [1] groups, [2] groups with a candidate, [4] sphere
+  // resolves (wave); BVH: [1] node iterations, [2] leaf-sphere iterations,
+  // [4] root resolutions (wave).  [3] resolves (lane), [5] node visits,
+  // [6] leaf sphere tests (lane).
   if (lane == 0) { atomicAdd(&segments[1], (unsigned long long)stats[0]); atomicAdd(&segments[2], (unsigned long long)stats[1]); atomicAdd(&segments[4], (unsigned long long)stats[3]); }
   atomicAdd(&segments[3], (unsigned long long)stats[2]);
   atomicAdd(&segments[5], (unsigned long long)bvh_stats[0]);
   atomicAdd(&segments[6], (unsigned long long)bvh_stats[1]);
+  atomicAdd(&segments[1], (unsigned long long)bvh_stats[2]);
+  atomicAdd(&segments[2], (unsigned long long)bvh_stats[3]);
+  atomicAdd(&segments[4], (unsigned long long)bvh_stats[4]);
 #endif
   RTMI_TRACE_END(n_taken)
   (void)n_taken;
@@ -611,7 +631,7 @@ __global__ __launch_bounds__(256) void debug_hit_kernel(const SpherePair *__rest
   const V3<float> d = mk(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
   float t0, t1;
 #if RTMI_STATS
-  unsigned st[4] = {0, 0, 0, 0}, bst[2] = {0, 0};
+  unsigned st[4] = {0, 0, 0, 0}, bst[5] = {0, 0, 0, 0, 0};
   out_idx[2 * i] = hit_world_packed<kPairGroup>(pairs, npairs, o, d, t0, st);
   out_idx[2 * i + 1] = acc.nnodes ? hit_world_bvh<kBigGroup>(acc, o, d, t1, bst) : -2;
 #else
@@ -863,12 +883,28 @@ RTMI_EXPORT int rt_ctx_destroy(rt_ctx *ctx) {
 namespace {
 constexpr size_t kBvhLdsMax = 64 * 1024;  // BVH bytes staged per block
 
-// BVH over the small spheres: median split on the longest centroid axis,
+// BVH over the small spheres: binary, SAH split (full sweep of the sorted
+// centroids on each axis: the split minimising area(L)*|L| + area(R)*|R|),
 // leaves of <= kLeafMax spheres, nodes in DFS order with skip links.  Boxes
 // are the spheres' double-precision bounds grown by a margin (1e-3 of the
 // scene scale, ~100x the float error of the sphere test at that scale) and
-// rounded outward to float, so every sphere the float test can report lies
-// strictly inside its leaf's box.
+// rounded outward to half precision, so every sphere the float test can
+// report lies strictly inside its leaf's box.
+uint16_t half_bits(_Float16 h) { return __builtin_bit_cast(uint16_t, h); }
+// largest half <= v (-inf below the half range)
+uint16_t half_down(double v) {
+  _Float16 h = _Float16(v);
+  while (double(h) > v) {
+    uint16_t b = half_bits(h);
+    if (b == 0x0000) b = 0x8001;          // +0 -> -min denormal
+    else if (b & 0x8000) b = uint16_t(b + 1);  // negative: away from zero
+    else b = uint16_t(b - 1);             // positive: toward zero
+    h = __builtin_bit_cast(_Float16, b);
+  }
+  return half_bits(h);
+}
+uint16_t half_up(double v) { return uint16_t(half_down(-v) ^ 0x8000); }
+
 struct BvhBuilder {
   const double *cr;
   const std::vector<float4> &g;
@@ -877,53 +913,67 @@ struct BvhBuilder {
   std::vector<float4> sph;
   std::vector<int32_t> idx;
 
-  void bounds(const int32_t *ids, int cnt, double lo[3], double hi[3]) const {
-    for (int a = 0; a < 3; ++a) { lo[a] = INFINITY; hi[a] = -INFINITY; }
-    for (int i = 0; i < cnt; ++i) {
-      const double *c = cr + 4 * ids[i];
-      const double rr = std::fabs(c[3]) + margin;
+  struct Box {
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    void add(const double *c, double rr) {
       for (int a = 0; a < 3; ++a) {
         lo[a] = std::min(lo[a], c[a] - rr);
         hi[a] = std::max(hi[a], c[a] + rr);
       }
     }
+    double area() const {
+      const double e0 = hi[0] - lo[0], e1 = hi[1] - lo[1], e2 = hi[2] - lo[2];
+      return e0 * e1 + e1 * e2 + e0 * e2;
+    }
+  };
+  Box bounds(const int32_t *ids, int cnt) const {
+    Box b;
+    for (int i = 0; i < cnt; ++i) b.add(cr + 4 * ids[i], std::fabs(cr[4 * ids[i] + 3]) + margin);
+    return b;
+  }
+  void sort_axis(int32_t *ids, int cnt, int ax) const {
+    std::sort(ids, ids + cnt, [&](int32_t x, int32_t y) {
+      const double cx = cr[4 * x + ax], cy = cr[4 * y + ax];
+      return cx < cy || (cx == cy && x < y);
+    });
   }
   void build(int32_t *ids, int cnt) {
     const int me = int(nodes.size());
     nodes.push_back(BvhNode{});
-    double lo[3], hi[3];
-    bounds(ids, cnt, lo, hi);
+    const Box bb = bounds(ids, cnt);
     BvhNode nd{};
-    for (int a = 0; a < 3; ++a) {
-      nd.bmin[a] = std::nextafter(float(lo[a]), -INFINITY);
-      nd.bmax[a] = std::nextafter(float(hi[a]), INFINITY);
-    }
+    nd.x = uint32_t(half_down(bb.lo[0])) | uint32_t(half_up(bb.hi[0])) << 16;
+    nd.y = uint32_t(half_down(bb.lo[1])) | uint32_t(half_up(bb.hi[1])) << 16;
+    nd.z = uint32_t(half_down(bb.lo[2])) | uint32_t(half_up(bb.hi[2])) << 16;
     if (cnt <= kLeafMax) {
-      nd.leaf = (int32_t(sph.size()) << 4) | cnt;
+      nd.link = ~((int32_t(sph.size()) << 4) | cnt);
       for (int i = 0; i < cnt; ++i) {
         sph.push_back(g[ids[i]]);
         idx.push_back(ids[i]);
       }
-      nd.skip = me + 1;
     } else {
-      double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
-      for (int i = 0; i < cnt; ++i)
-        for (int a = 0; a < 3; ++a) {
-          clo[a] = std::min(clo[a], cr[4 * ids[i] + a]);
-          chi[a] = std::max(chi[a], cr[4 * ids[i] + a]);
+      // SAH sweep: prefix/suffix boxes over the centroid order of each axis
+      double best = INFINITY;
+      int best_ax = 0, best_mid = cnt / 2;
+      std::vector<double> left_cost(cnt);
+      for (int ax = 0; ax < 3; ++ax) {
+        sort_axis(ids, cnt, ax);
+        Box l;
+        for (int i = 1; i < cnt; ++i) {
+          l.add(cr + 4 * ids[i - 1], std::fabs(cr[4 * ids[i - 1] + 3]) + margin);
+          left_cost[i] = l.area() * i;
         }
-      int ax = 0;
-      for (int a = 1; a < 3; ++a)
-        if (chi[a] - clo[a] > chi[ax] - clo[ax]) ax = a;
-      const int mid = cnt / 2;
-      std::nth_element(ids, ids + mid, ids + cnt, [&](int32_t x, int32_t y) {
-        const double cx = cr[4 * x + ax], cy = cr[4 * y + ax];
-        return cx < cy || (cx == cy && x < y);
-      });
-      build(ids, mid);
-      build(ids + mid, cnt - mid);
-      nd.leaf = -1;
-      nd.skip = int(nodes.size());
+        Box r;
+        for (int i = cnt - 1; i >= 1; --i) {
+          r.add(cr + 4 * ids[i], std::fabs(cr[4 * ids[i] + 3]) + margin);
+          const double c = left_cost[i] + r.area() * (cnt - i);
+          if (c < best) { best = c; best_ax = ax; best_mid = i; }
+        }
+      }
+      sort_axis(ids, cnt, best_ax);
+      build(ids, best_mid);
+      build(ids + best_mid, cnt - best_mid);
+      nd.link = int32_t(nodes.size());
     }
     nodes[me] = nd;
   }
@@ -1051,7 +1101,7 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
     // the BVH must fit in LDS beside the accumulators; otherwise it is not
     // offered (RT_ACCEL_BVH renders brute force)
     const size_t lds = bvh_lds_bytes(int32_t(b.nodes.size()), int32_t(b.sph.size()));
-    ctx->nnodes = lds <= kBvhLdsMax ? int32_t(b.nodes.size()) : 0;
+    ctx->nnodes = lds <= kBvhLdsMax && n <= 65535 ? int32_t(b.nodes.size()) : 0;
     int per_cu = 0;
     if (ctx->nnodes)
       HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<8, true, true>,

@@ -582,17 +582,20 @@ __device__ __forceinline__ int32_t hit_world_packed(const SpherePair *__restrict
 // float error, rtmi_device.hip build_bvh), so a culled sphere is one the
 // brute-force loop would have rejected.  Large spheres (the R=1000 ground,
 // which bounds everything) stay in a brute-force packed list ("big").
+// One node = 16 bytes = one ds_read_b128: per axis the box's lo and hi as
+// IEEE halves in one dword (lo in bits 0-15), rounded OUTWARD from the
+// double bounds (a half box contains the float box it replaces, so culling
+// stays conservative; the slab test converts them for free with
+// v_fma_mix_f32), and a link: >= 0 for an inner node = the skip index (next
+// node when the box is missed; the first child is index + 1), < 0 for a
+// leaf = ~(first << 4 | count) (the next node is index + 1 either way).
 struct BvhNode {
-  float bmin[3];
-  int32_t skip;  // next node when this subtree is not entered (DFS order; leaf: index + 1)
-  float bmax[3];
-  int32_t leaf;  // -1: inner node (first child = index + 1); else first << 4 | count (1..kLeafMax)
+  uint32_t x, y, z;
+  int32_t link;
 };
+static_assert(sizeof(BvhNode) == 16, "BVH node is one 16-byte LDS read");
 #ifndef RTMI_BVH_LEAF
 #define RTMI_BVH_LEAF 4
-#endif
-#ifndef RTMI_BOX_FMA
-#define RTMI_BOX_FMA 1
 #endif
 constexpr int kLeafMax = RTMI_BVH_LEAF;
 #ifndef RTMI_BIG_FACTOR
@@ -617,20 +620,20 @@ struct Accel {
 
 // The BVH lives in LDS during a launch (dynamic shared memory, staged by
 // every block at its start): the traversal is a chain of dependent node
-// loads, ~100 cycles from LDS against ~500+ from L2.  Layout: nodes as
-// 2*nnodes float4, then nsph sphere float4s, then nsph int32 indices.
+// loads, ~100 cycles from LDS against ~500+ from L2.  Layout: nnodes 16-byte
+// nodes, then nsph sphere float4s, then nsph uint16 scene indices (the BVH is
+// only offered for scenes of < 65536 spheres).
 extern __shared__ float4 rtmi_bvh_lds[];
 __host__ __device__ constexpr size_t bvh_lds_bytes(int32_t nnodes, int32_t nsph) {
-  return size_t(2 * nnodes + nsph) * 16 + size_t(nsph) * 4;
+  return size_t(nnodes + nsph) * 16 + size_t(nsph) * 2;
 }
 
 __device__ __forceinline__ void stage_bvh(const Accel &g) {
-  // nodes split into a lo[] and a hi[] array (independent LDS loads)
   const float4 *nodes = reinterpret_cast<const float4 *>(g.nodes);
-  for (int i = threadIdx.x; i < 2 * g.nnodes; i += blockDim.x) rtmi_bvh_lds[(i & 1) * g.nnodes + (i >> 1)] = nodes[i];
-  for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) rtmi_bvh_lds[2 * g.nnodes + i] = g.sph[i];
-  int32_t *idx = reinterpret_cast<int32_t *>(rtmi_bvh_lds + 2 * g.nnodes + g.nsph);
-  for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) idx[i] = g.sph_idx[i];
+  for (int i = threadIdx.x; i < g.nnodes; i += blockDim.x) rtmi_bvh_lds[i] = nodes[i];
+  for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) rtmi_bvh_lds[g.nnodes + i] = g.sph[i];
+  uint16_t *idx = reinterpret_cast<uint16_t *>(rtmi_bvh_lds + g.nnodes + g.nsph);
+  for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) idx[i] = uint16_t(g.sph_idx[i]);
   __syncthreads();
 }
 
@@ -651,6 +654,9 @@ __device__ __forceinline__ int32_t hit_world_bvh(const Accel &acc_s, V3<float> o
   int32_t best = -1;
   // sphere.h:30-38 root logic; tie rule order-independent (see above)
   auto resolve = [&](int32_t idx, float hb, float disc) {
+#if RTMI_STATS
+    if (__lane_id() == __builtin_ctzll(__ballot(1))) bstats[4] += 1;
+#endif
     const float sq = dsqrt(disc);
     float root = (-hb - sq) * inv_a;
     bool ok = !(root < t_min) && (root < t_max || (root == t_max && idx > best));
@@ -697,8 +703,8 @@ __device__ __forceinline__ int32_t hit_world_bvh(const Accel &acc_s, V3<float> o
   }
   // 2. the BVH (staged in LDS by stage_bvh), stackless: per-lane walk of the
   // DFS node array with skip links
-  const float4 *lds_sph = rtmi_bvh_lds + 2 * acc_s.nnodes;
-  const int32_t *lds_idx = reinterpret_cast<const int32_t *>(rtmi_bvh_lds + 2 * acc_s.nnodes + acc_s.nsph);
+  const float4 *lds_sph = rtmi_bvh_lds + acc_s.nnodes;
+  const uint16_t *lds_idx = reinterpret_cast<const uint16_t *>(rtmi_bvh_lds + acc_s.nnodes + acc_s.nsph);
   // inverse direction with |d_i| clamped to >= 1e-20: no infinities, so no
   // 0*inf or inf-inf NaNs in the slab test (min/max would not ignore them
   // reliably).  The clamp moves the ray by a negligible angle; a ray running
@@ -706,53 +712,50 @@ __device__ __forceinline__ int32_t hit_world_bvh(const Accel &acc_s, V3<float> o
   // sits at least the box margin inside every face.
   auto safe_inv = [](float v) { return 1.0f / (__builtin_fabsf(v) < 1e-20f ? __builtin_copysignf(1e-20f, v) : v); };
   const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
-#if RTMI_BOX_FMA
   // slab distances as one fma per plane: (b - o) * i = fma(b, i, -o*i); the
   // box margin covers the different rounding
   const float ox = -o.x * ix, oy = -o.y * iy, oz = -o.z * iz;
-#endif
-  const float4 *lds_lo = rtmi_bvh_lds, *lds_hi = rtmi_bvh_lds + acc_s.nnodes;
+  const uint4 *lds_node = reinterpret_cast<const uint4 *>(rtmi_bvh_lds);
+  auto lo16 = [](uint32_t w) { return float(__builtin_bit_cast(_Float16, uint16_t(w))); };
+  auto hi16 = [](uint32_t w) { return float(__builtin_bit_cast(_Float16, uint16_t(w >> 16))); };
   int32_t node = 0;
   while (node < acc_s.nnodes) {
-    const float4 lo = lds_lo[node];
-    const float4 hi = lds_hi[node];
-#if RTMI_BOX_FMA
-    const float tx0 = __builtin_fmaf(lo.x, ix, ox), tx1 = __builtin_fmaf(hi.x, ix, ox);
-    const float ty0 = __builtin_fmaf(lo.y, iy, oy), ty1 = __builtin_fmaf(hi.y, iy, oy);
-    const float tz0 = __builtin_fmaf(lo.z, iz, oz), tz1 = __builtin_fmaf(hi.z, iz, oz);
-#else
-    const float tx0 = (lo.x - o.x) * ix, tx1 = (hi.x - o.x) * ix;
-    const float ty0 = (lo.y - o.y) * iy, ty1 = (hi.y - o.y) * iy;
-    const float tz0 = (lo.z - o.z) * iz, tz1 = (hi.z - o.z) * iz;
-#endif
+    const uint4 nd = lds_node[node];
+    const float tx0 = __builtin_fmaf(lo16(nd.x), ix, ox), tx1 = __builtin_fmaf(hi16(nd.x), ix, ox);
+    const float ty0 = __builtin_fmaf(lo16(nd.y), iy, oy), ty1 = __builtin_fmaf(hi16(nd.y), iy, oy);
+    const float tz0 = __builtin_fmaf(lo16(nd.z), iz, oz), tz1 = __builtin_fmaf(hi16(nd.z), iz, oz);
     // slab interval clipped to [0, t_max].  No slack is needed: a sphere
     // that can be hit lies >= the box margin inside the box, so its chord
     // starts after tnear and ends before tfar by far more than rounding, and
     // a hit at t_hit >= 0.001 with t_hit <= t_max (ties included) keeps the
-    // box entered.
+    // box entered.  Half-precision bounds only make the box larger.
     const float tnear = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx0, tx1), __builtin_fminf(ty0, ty1)),
                                         __builtin_fmaxf(__builtin_fminf(tz0, tz1), 0.0f));
     const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx0, tx1), __builtin_fmaxf(ty0, ty1)),
                                        __builtin_fminf(__builtin_fmaxf(tz0, tz1), t_max));
     const bool enter = tnear <= tfar;
-    const int32_t leaf = __float_as_int(hi.w);
+    const int32_t link = int32_t(nd.w);
 #if RTMI_STATS
     bstats[0] += 1;
+    if (__lane_id() == __builtin_ctzll(__ballot(1))) bstats[2] += 1;
 #endif
-    if (enter && leaf >= 0) {
-      const int32_t first = leaf >> 4, cnt = leaf & 15;
+    if (enter && link < 0) {
+      const int32_t first = (~link) >> 4, cnt = (~link) & 15;
 #if RTMI_STATS
       bstats[1] += cnt;
 #endif
       for (int32_t k = first; k < first + cnt; ++k) {
+#if RTMI_STATS
+        if (__lane_id() == __builtin_ctzll(__ballot(1))) bstats[3] += 1;
+#endif
         const float4 s = lds_sph[k];
         const float hb = __builtin_fmaf(-s.x, d.x, __builtin_fmaf(-s.y, d.y, __builtin_fmaf(-s.z, d.z, K)));
         const float acc = __builtin_fmaf(mx, s.x, __builtin_fmaf(my, s.y, __builtin_fmaf(mz, s.z, __builtin_fmaf(a, s.w, aL))));
         const float disc = __builtin_fmaf(hb, hb, -acc);
-        if (!(disc < 0.0f)) resolve(lds_idx[k], hb, disc);
+        if (!(disc < 0.0f)) resolve(int32_t(lds_idx[k]), hb, disc);
       }
     }
-    node = enter ? node + 1 : __float_as_int(lo.w);
+    node = (enter || link < 0) ? node + 1 : link;
   }
   t_hit = t_max;
   return best;

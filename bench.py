@@ -28,7 +28,9 @@ cpu_baseline: the reference itself (oracle/_ref/ref_harness: worker() at -O2,
 16 std::threads as the reference's concurrency) on a bounded sample, rank 0,
 N = 1 only.
 
---workload selects a secondary line (not the headline): nw_motion_blur = the
+--workload config4 / config5 time BASELINE's other final-scene configs
+(1200x800 at 5000 spp; 3840x2160 at 2000 spp).  It also selects the
+Next-Week lines (not the headline): nw_motion_blur = the
 Next-Week random scene with moving spheres at 1200x800x500 (the reference's
 only published Next-Week number, rt_next_week/cuda/README.md:167-174: 37.88 s),
 nw_final = the Next-Week final scene at 800x800 (main.cu:517-524; --nw-spp,
@@ -51,6 +53,11 @@ FLOP_PER_SPHERE_TEST = 18
 PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector (MI355X_MICROARCH.md)
 PUBLISHED_CPU_MSPS = 0.1189  # README.md:16-19: rt_in_one_weekend, 1200x800x500, 16 threads, 4036.1 s
 METRIC = "Msamples/sec (pixels x spp) on RTIOW final scene"
+# BASELINE.json configs on the final scene: config2 = the headline (1 GPU,
+# 1200x800x500); config4 = the same at 5000 spp; config5 = 3840x2160 (16:9
+# camera) at 2000 spp (quoted for 8 GPUs; the final scene has the
+# reference's defocus blur, aperture 0.1).
+RTIOW_WORKLOADS = {"config2": (1200, 800, 500), "config4": (1200, 800, 5000), "config5": (3840, 2160, 2000)}
 
 
 def cpu_baseline(threads=16):
@@ -101,13 +108,14 @@ def main():
                     help="closest-hit search: bvh (default; same image bit for bit) or brute force")
     ap.add_argument("--ordering", choices=["cost", "none"], default="cost")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["config2", "nw_motion_blur", "nw_final"], default="config2")
+    ap.add_argument("--workload", choices=list(RTIOW_WORKLOADS) + ["nw_motion_blur", "nw_final"], default="config2")
     ap.add_argument("--nw-spp", type=int, default=0, help="spp of the nw_* workloads (default: 500 / 1024)")
     ap.add_argument("--strip-of", type=int, default=0,
                     help="analysis only: time ONE rank's interleaved strip of an N-GPU run on this GPU")
     args = ap.parse_args()
-    if args.workload != "config2":
+    if args.workload.startswith("nw_"):
         return bench_nw(args)
+    W, H, SPP = RTIOW_WORKLOADS[args.workload]
 
     import torch
     import torch.distributed as dist
@@ -215,7 +223,7 @@ def main():
         achieved = flop_rank / (kernel_ms * 1e-3) / 1e12
         traffic = None
         pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
+        if os.path.exists(pmc) and args.workload == "config2" and not args.strip_of:  # measured on config 2
             try:
                 traffic = (json.load(open(pmc)).get(args.accel) or {}).get("hbm_bytes_per_launch")
             except Exception:
@@ -234,7 +242,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic: RTIOW final scene regenerated from glibc rand() seed 1 (487 spheres, = reference)",
             "config": {
-                "workload": "rtiow_final_1200x800_500spp_depth50",
+                "workload": f"rtiow_final_{W}x{H}_{SPP}spp_depth{DEPTH}",
                 "width": W, "height": H, "spp": SPP, "max_depth": DEPTH, "seed": SEED, "spheres": len(world),
                 "partition": "interleaved rows, one RCCL gather" if N > 1 else "single GPU",
                 "tile": f"{args.tile_w}x{64 // args.tile_w}",

@@ -308,10 +308,13 @@ def test_bvh_learn_scene_edge_cases(learn_renderer):
         assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("seed", [1, 2, 3])
-def test_bvh_random_scenes_equal_brute_force(seed):
+@pytest.mark.parametrize("seed,scale,shift", [(1, 1.0, 0.0), (2, 1.0, 0.0), (3, 1.0, 0.0), (4, 3000.0, 50000.0)])
+def test_bvh_random_scenes_equal_brute_force(seed, scale, shift):
     """Random scenes: radii over three decades, overlaps, hollow (negative
-    radius) spheres, huge spheres, coincident centres; BVH == brute force."""
+    radius) spheres, huge spheres, coincident centres; BVH == brute force.
+    The last case is scaled and shifted so that node bounds leave the half
+    range (boxes stored as halves rounded outward become infinite on that
+    side) and lose most of their precision: still the same image."""
     g = np.random.default_rng(seed)
     n = 300
     c = g.uniform(-8, 8, (n, 3))
@@ -326,8 +329,11 @@ def test_bvh_random_scenes_equal_brute_force(seed):
     cr = np.vstack([[0, -1000, 0, 1000], [0, 1, 40, 30], cr])  # ground + one more big sphere
     kinds = np.concatenate([[0, 1], kinds]).astype(np.int32)
     params = np.vstack([[0.5, 0.5, 0.5, 0], [0.7, 0.6, 0.5, 0.1], params])
+    cr = cr * scale
+    cr[:, 0] += shift
     world = rt.World(cr, kinds, params)
-    cam = rt.camera((13, 2, 3), (0, 0, 0), (0, 1, 0), 40.0, 1.5, 0.1, 10.0)
+    look_from = (13 * scale + shift, 2 * scale, 3 * scale)
+    cam = rt.camera(look_from, (shift, 0, 0), (0, 1, 0), 40.0, 1.5, 0.1 * scale, 10.0 * scale)
     r_ = rt.Renderer(world, 0)
     try:
         want = r_.render(cam, 72, 48, 6, 50, SEED)

@@ -19,3 +19,6 @@ L.rt_ctx_debug_counters(r._h, v)
 segs = v[0]
 print(f"segments {segs}; per lane-segment: node visits {v[5] / segs:.2f}, leaf sphere tests {v[6] / segs:.2f}, "
       f"resolves {v[3] / segs:.2f}")
+ws = segs / 64.0  # wave-segments (lane utilisation ~0.997)
+print(f"per wave-segment: node iterations {v[1] / ws:.2f}, leaf-sphere iterations {v[2] / ws:.2f}, "
+      f"root-resolution blocks {v[4] / ws:.2f}")

@@ -60,6 +60,28 @@ METRIC = "Msamples/sec (pixels x spp) on RTIOW final scene"
 RTIOW_WORKLOADS = {"config2": (1200, 800, 500), "config4": (1200, 800, 5000), "config5": (3840, 2160, 2000)}
 
 
+def dist_setup(torch, dist):
+    """One process per GPU (torch.distributed.run env).  RCCL ("nccl") is the
+    product path.  RTMI_DIST_BACKEND=gloo is a rehearsal mode for a box with
+    fewer GPUs than ranks: ranks share devices (local_rank % device count) and
+    the collectives run on host copies; the timed region then includes those
+    copies, so it is never a reported number."""
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("RTMI_DIST_BACKEND", "nccl")
+    device = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
+    torch.cuda.set_device(device)
+    dev = torch.device("cuda", device)
+    if world_size > 1:
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    coll = dev if backend == "nccl" else torch.device("cpu")
+    return world_size, rank, device, dev, coll
+
+
 def cpu_baseline(threads=16):
     """The reference's own worker() (oracle/_ref/ref_harness bench) on a
     bounded sample: full 1200x800 image at 4 spp (~3.8 M samples)."""
@@ -123,16 +145,10 @@ def main():
     import a_dive_into_ray_tracing_amd as rt
     from a_dive_into_ray_tracing_amd import dist as rdist
 
-    world_size = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    world_size, rank, local_rank, dev, coll = dist_setup(torch, dist)
     if world_size != args.gpus:
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE {world_size}", file=sys.stderr)
     N = world_size
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    if N > 1:
-        dist.init_process_group("nccl", device_id=dev)
 
     world = rt.random_scene()
     cam = rt.final_camera(W / H)
@@ -163,7 +179,7 @@ def main():
             e1.record(stream)
             ev.append((e0, e1))
         if N > 1:  # the single exchange step: strips -> rank 0 over RCCL/xGMI
-            gathered = rdist.gather_strips(strip, rank, N, dst=0)
+            gathered = rdist.gather_strips(strip if coll.type == "cuda" else strip.cpu(), rank, N, dst=0)
 
     for _ in range(args.warmup):
         step(False)
@@ -180,17 +196,17 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if N > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     segs = r.last_segments()  # this rank's strip, last render
     if N > 1:
-        t = torch.tensor([segs], dtype=torch.float64, device=dev)
+        t = torch.tensor([segs], dtype=torch.float64, device=coll)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         total_segs = float(t.item())
-        km = torch.tensor([kernel_ms], dtype=torch.float64, device=dev)
+        km = torch.tensor([kernel_ms], dtype=torch.float64, device=coll)
         dist.all_reduce(km, op=dist.ReduceOp.MAX)
         kernel_ms_max = float(km.item())
     else:
@@ -289,14 +305,7 @@ def bench_nw(args):
     import a_dive_into_ray_tracing_amd.nextweek as nw
     from a_dive_into_ray_tracing_amd import dist as rdist
 
-    world_size = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    N = world_size
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    if N > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    N, rank, local_rank, dev, coll = dist_setup(torch, dist)
     if args.workload == "nw_motion_blur":
         which, Wn, Hn, spp = 1, 1200, 800, args.nw_spp or 500
         earth = None
@@ -320,7 +329,7 @@ def bench_nw(args):
             e1.record(stream)
             ev.append((e0, e1))
         if N > 1:
-            rdist.gather_strips(strip, rank, N, dst=0)
+            rdist.gather_strips(strip if coll.type == "cuda" else strip.cpu(), rank, N, dst=0)
 
     for _ in range(args.warmup):
         step(False)
@@ -337,7 +346,7 @@ def bench_nw(args):
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if N > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))

@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -59,6 +60,10 @@ struct RenderArgs {
   // chunks of chunk1, phase 2 = [spp1, spp) in chunks of chunk2; phase-2 items
   // come last in the grid, so the dispatch tail is one short item
   int32_t tiles, spp1, chunk1, nch1, chunk2, nch2;
+  // grid kernel: every block's items share one tile (nch1 a multiple of the
+  // block's waves, no phase 2), so the block sums its waves' accumulators and
+  // flushes once (a quarter of the global atomics)
+  int32_t block_flush;
   // progressive passes: this launch renders samples s_base + [0, spp)
   int32_t s_base;
   uint64_t out_elems;  // elements of accum / out (RTMI_CHECK builds verify every write)
@@ -310,6 +315,22 @@ __global__ __launch_bounds__(64 * GridShape<BVH>::waves, GridShape<BVH>::per_eu)
   atomicAdd(&segments[4], (unsigned long long)bvh_stats[4]);
 #endif
   RTMI_TRACE_END(1)
+  if constexpr (CHUNKED) {
+    if (a.block_flush) {  // block-uniform; no wave of this block returned early
+      __syncthreads();
+      if (wave == 0 && lane < nv) {
+        const int ly = lane / vw, lx = lane - ly * vw;
+        const size_t o3 = (size_t(y0 + ly) * size_t(a.W) + size_t(x0 + lx)) * 3;
+        for (int c = 0; c < 3; ++c) {
+          unsigned long long v = 0;
+#pragma unroll
+          for (int w = 0; w < WPB; ++w) v += acc[w][c][lane];
+          atomicAdd(&accum[o3 + c], v);
+        }
+      }
+      return;
+    }
+  }
   if (lane < nv) {
     const int ly = lane / vw, lx = lane - ly * vw;
     const size_t o3 = (size_t(y0 + ly) * size_t(a.W) + size_t(x0 + lx)) * 3;
@@ -758,6 +779,9 @@ struct rt_ctx {
   // cost-ordered dispatch: per-tile world.hit counts of the
   // last render with the same tile layout order the next one's tiles
   int32_t ordering = RT_ORDER_COST;
+  // block-level accumulator flush of the automatic grid schedule (same image;
+  // RTMI_BLOCK_FLUSH=0 in the environment turns it off, for A/B and tests)
+  bool block_flush = !(std::getenv("RTMI_BLOCK_FLUSH") && std::getenv("RTMI_BLOCK_FLUSH")[0] == '0');
   unsigned *cost_prev = nullptr, *cost_cur = nullptr, *cost_sorted = nullptr;
   int32_t *order = nullptr, *iota = nullptr;
   size_t cost_cap = 0;  // tiles
@@ -1242,6 +1266,14 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   chunk1 = std::min(chunk1, spp);
   tail = std::min(tail, spp);
   const int32_t spp1 = spp - tail;
+  const int64_t grid_wpb = bvh ? GridShape<true>::waves : GridShape<false>::waves;
+  if (ctx->chunk <= 0 && !persistent && tail == 0 && spp1 >= grid_wpb) {
+    // automatic grid schedule: a multiple of the block's waves per tile, so a
+    // block's items share a tile and it flushes once (block_flush)
+    int64_t n1 = (spp1 + chunk1 - 1) / chunk1;
+    n1 = (n1 + grid_wpb - 1) / grid_wpb * grid_wpb;
+    chunk1 = int32_t((spp1 + n1 - 1) / n1);
+  }
   const int32_t nch1 = spp1 > 0 ? (spp1 + chunk1 - 1) / chunk1 : 0;
   chunk2 = std::min(chunk2, std::max(tail, 1));
   const int32_t nch2 = tail > 0 ? (tail + chunk2 - 1) / chunk2 : 0;
@@ -1255,6 +1287,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   a.row0 = row0; a.row_step = row_step; a.nrows_valid = nvalid;
   a.tiles_x = tiles_x; a.n_items = int32_t(items);
   a.tiles = int32_t(tiles); a.spp1 = spp1; a.chunk1 = chunk1; a.nch1 = nch1; a.chunk2 = chunk2; a.nch2 = nch2;
+  a.block_flush = !persistent && nch2 == 0 && nch1 % grid_wpb == 0 && ctx->block_flush;
   a.s_base = s_base;
   a.out_elems = uint64_t(nvalid) * uint64_t(W) * 3;
   const bool chunked = pass_accum || nch1 + nch2 > 1;

@@ -411,3 +411,25 @@ def test_cost_ordered_dispatch_same_image(kernel, accel, final_world, final_rend
     assert np.array_equal(first, plain) and np.array_equal(again, plain)
     want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, 2 * S, 50, SEED + 1)
     assert np.array_equal(ordered, want)
+
+
+@pytest.mark.parametrize("accel", ["none", "bvh"])
+def test_block_flush_same_image(accel, final_world, monkeypatch):
+    """The automatic grid schedule gives every block the items of one tile and
+    flushes the block's summed accumulators once; RTMI_BLOCK_FLUSH=0 flushes
+    per wave.  Same image bit for bit, and equal to the oracle."""
+    W, H, S = 40, 24, 37  # 37 spp: 4 items of 10/10/10/7 samples per tile
+    cam = rt.final_camera(W / H)
+    imgs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("RTMI_BLOCK_FLUSH", flag)
+        r = rt.Renderer(final_world, 0)
+        try:
+            r.set_kernel("grid")
+            r.set_accel(accel)
+            imgs.append(r.render(cam, W, H, S, 50, SEED))
+        finally:
+            r.close()
+    assert np.array_equal(imgs[0], imgs[1])
+    want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
+    assert np.array_equal(imgs[0], want)

@@ -145,7 +145,7 @@ static void flatten(int oct, int ordered, int n, int *pos) {
   f->skip = *pos;
 }
 
-typedef struct { long visits, tests, wave_iters, wave_leaf_iters, waves, res_blocks, res_lanes, res_acc, res_blocks_pf; } Stat;
+typedef struct { long visits, tests, wave_iters, wave_leaf_iters, waves, res_blocks, res_lanes, res_acc, res_blocks_pf, pair_iters; } Stat;
 
 static void run(const char *name, int ordered) {
   /* small spheres only, as the kernel: big (r > 4 x median) stay brute force */
@@ -265,11 +265,15 @@ static void run(const char *name, int ordered) {
         }
         node[l] = enter ? node[l] + 1 : f->skip;
       }
-      if (active) { st.wave_iters++; if (anyleaf) st.wave_leaf_iters += maxcnt; }
+      if (active) { st.wave_iters++; if (anyleaf) { st.wave_leaf_iters += maxcnt; st.pair_iters += (maxcnt + 1) / 2; } }
       for (int i = 0; i < 16; i++) { st.res_blocks += cand[i]; st.res_blocks_pf += candpf[i]; }
     }
     st.waves++;
   }
+  if (!g_spec) printf("   pair-iters/wave-seg %.2f  cost(node 24, sphere 13, pair 16, resolve 45): scalar %.0f  packed %.0f\n",
+         (double)st.pair_iters*64/nseg,
+         ((double)st.wave_iters*24 + st.wave_leaf_iters*13 + st.res_blocks*45)*64/nseg,
+         ((double)st.wave_iters*24 + st.pair_iters*16 + st.res_blocks*45)*64/nseg);
   if (!g_spec) printf("   resolve blocks/wave-seg %.2f (after a t_max prefilter %.2f); lane candidates/seg %.2f accepted %.2f\n",
          (double)st.res_blocks*64/nseg, (double)st.res_blocks_pf*64/nseg, (double)st.res_lanes/nseg, (double)st.res_acc/nseg);
   printf("%s%-26s nodes %4d  lane visits %6.2f  leaf tests %5.2f  wave iters %6.2f  wave leaf-iters %6.2f  (per segment)\n",
@@ -333,7 +337,7 @@ int main(int argc, char **argv) {
   printf("segments %d\n", nseg);
   if (getenv("F16")) g_f16 = 1;
   for (g_spec = 0; g_spec < 2; g_spec++)
-  for (int lm = 1; lm <= 8; lm *= 2) {
+  for (int lm = 1; lm <= 12; lm += (lm < 2 ? 1 : 2)) {
     if (g_spec) printf("-- speculative (leaves postponed until every lane holds one)\n");
     char nm[64];
     g_leafmax = lm; g_sah = 0; sprintf(nm, "median leaf%d fixed", lm); run(nm, 0);

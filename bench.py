@@ -294,6 +294,45 @@ def main():
 
 
 NW_PUBLISHED_MSPS = 1200 * 800 * 500 / 37.8792 / 1e6  # rt_next_week/cuda/README.md:167-174 (RTX 2060 Max-Q)
+# Algorithmic FLOP of one miss test per Next-Week object kind (the reference's
+# hit functions): sphere.h 18 (as the RTIOW count, |d|^2
+# hoisted); moving_sphere.h center(t) 12 + 18; aarect.h t, two coordinates 6;
+# box.h = its six rects 36; constant_medium.h its boundary twice + 4; and per
+# instance (translate + rotate_y of the ray) 15.
+NW_FLOP = {0: 18, 1: 30, 2: 6, 3: 6, 4: 6, 5: 36}
+NW_FLOP_INSTANCE = 15
+
+
+def nw_flop_per_segment(flat):
+    """Brute-force-equivalent FLOP of one world.hit over the flattened scene."""
+    obj = flat["obj"].view(np.int32).reshape(-1, 16)
+    kind, aux = obj[:, 12], obj[:, 15]
+    total = 0
+    for k, a in zip(kind, aux):
+        total += NW_FLOP[int(k)] if k != 6 else 2 * NW_FLOP[int(a) & 255] + 4
+    return total + NW_FLOP_INSTANCE * (flat["inst"].size // 8)
+
+
+def nw_cpu_baseline(flat, cam, which, W, H):
+    """The oracle's Next-Week restatement (C, OpenMP, brute force over the
+    objects: the CPU port, the reference being CUDA only) on a bounded
+    sample of the same scene: 40 evenly spaced rows."""
+    try:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_py as O
+
+        spp = 20 if which == 8 else 160  # ~10-15 s on the GPU box's 16 host threads
+        rows = 40
+        t0 = time.perf_counter()
+        O.nw_render(flat, cam, W, H, spp, DEPTH, SEED, row0=0, row_step=H // rows, nrows=rows)
+        dt = time.perf_counter() - t0
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        return {"value": round(rows * W * spp / dt / 1e6, 5), "unit": "Msamples/s", "cores": threads, "kind": "port",
+                "sample": f"oracle Next-Week C restatement (brute force over objects), {rows} rows x {W} x {spp} spp "
+                          f"({dt:.1f} s wall, OpenMP)"}
+    except Exception as e:
+        print(f"bench: nw cpu baseline unavailable: {e}", file=sys.stderr)
+        return None
 
 
 def bench_nw(args):
@@ -351,6 +390,9 @@ def bench_nw(args):
         elapsed = float(t.item())
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     segs = r.last_segments()
+    flop_seg = nw_flop_per_segment(scene.flat())
+    flop_rank = segs * flop_seg  # this rank's launch
+    achieved = flop_rank / (kernel_ms * 1e-3) / 1e12
     if rank == 0:
         samples = Wn * Hn * spp
         value = samples * args.steps / elapsed / 1e6
@@ -364,13 +406,22 @@ def bench_nw(args):
             "config": {"workload": f"{args.workload}_{Wn}x{Hn}_{spp}spp_depth{DEPTH}", "scene": which, "width": Wn,
                        "height": Hn, "spp": spp, "max_depth": DEPTH, "seed": SEED,
                        "partition": "interleaved rows, one RCCL gather" if N > 1 else "single GPU"},
-            "roofline": None,
+            "roofline": {
+                "bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                "flop_per_launch": flop_rank, "flop_per_segment": flop_seg, "segments_per_launch": segs,
+                "kernel_ms": round(kernel_ms, 3), "work_equivalent": True,
+                "note": "brute-force-equivalent FLOP (every object's miss test per world.hit, bench.NW_FLOP) over the "
+                        "BVH kernel's time, as SURVEY 8(d) prescribes for culling: frac can exceed 1",
+            },
             "kernel_ms": round(kernel_ms, 3),
             "segments_per_sample_rank0": round(segs / (nrows * Wn * spp), 4),
             "objects_bvh_nodes": list(r.info()),
             "vs_baseline_ref": "reference rt_next_week CUDA, random_scene with moving spheres 1200x800x500 in 37.88 s "
                                "(RTX 2060 Max-Q): 12.67 Msamples/s",
         }
+        if N == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = nw_cpu_baseline(scene.flat(), cam, which, Wn, Hn)
         print(json.dumps(line), flush=True)
     r.close()
     if N > 1:

@@ -139,3 +139,40 @@ def test_cli_matches_library(tmp_path, earth):
         mean = (sums / np.float32(spp)).astype(np.float32)
         want = np.floor(255.99 * np.sqrt(mean).astype(np.float32).astype(np.float64)).astype(np.int64)[::-1]
         assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("shutter", [(0.0, 1.0), (0.3, 0.6)])
+def test_moving_spheres_bit_exact(shutter):
+    """Moving spheres with their own time ranges inside and outside the
+    shutter (the centre extrapolates linearly; their BVH boxes are swept over
+    [0, 1]), under translate/rotate_y instances and as a medium's boundary:
+    equal to the oracle (brute force), world.hit counts included."""
+    g = np.random.default_rng(7)
+    s = nw.Scene()
+    gray = s.lambertian(s.solid(0.5, 0.5, 0.5))
+    s.add(s.sphere((0, -1000, 0), 1000, gray))
+    kids = []
+    for k in range(150):
+        c0 = (g.uniform(-6, 6), g.uniform(0.1, 1.5), g.uniform(-6, 6))
+        c1 = (c0[0] + g.uniform(-1, 1), c0[1] + g.uniform(0, 1.2), c0[2] + g.uniform(-1, 1))
+        t0, t1 = [(0.0, 1.0), (0.2, 0.7), (-0.5, 0.5), (0.4, 2.0)][k % 4]
+        mat = [gray, s.metal(s.solid(0.8, 0.7, 0.6), 0.2), s.dielectric(1.5)][k % 3]
+        obj = s.moving_sphere(c0, c1, t0, t1, g.uniform(0.1, 0.4), mat)
+        if k % 5 == 0:
+            kids.append(obj)  # instanced below
+        else:
+            s.add(obj)
+    inst = s.translate(s.rotate_y(s.group(kids), 25.0), (1.0, 0.2, -0.5))
+    s.add(inst)
+    fog = s.constant_medium(s.moving_sphere((2, 1, 2), (2, 1.5, 2.5), 0.0, 1.0, 0.8, gray), 0.5, s.solid(0.9, 0.9, 0.9))
+    s.add(fog)
+    s.add(s.box((-2, 0, -2), (-1, 1, -1), gray))
+    s.set_background(0.7, 0.8, 1.0)
+    W, H, spp = 40, 30, 6
+    cam = nw.camera((13, 2, 3), (0, 0, 0), (0, 1, 0), 30.0, W / H, 0.1, 10.0, *shutter)
+    r = nw.NwRenderer(s)
+    got, segs = r.render(cam, W, H, spp, 50, SEED), r.last_segments()
+    r.close()
+    want, want_segs = O.nw_render(s.flat(), cam, W, H, spp, 50, SEED)
+    assert np.array_equal(got, want), f"max |d| {np.abs(got - want).max()}"
+    assert segs == want_segs

@@ -346,12 +346,12 @@ int flatten(rt_nw_scene *s) {
 // (the R=1000 ground sphere) ends up alone near the root instead of inflating
 // every box on its path, as a median split leaves it.  Leaves of <=
 // kNodeLeafMax objects, DFS order with skip links.  Boxes are the objects'
-// double bounds grown by 1e-3 of the scene scale and rounded outward to float
+// double bounds, each grown by its own margin, rounded outward to float
 // (the RTIOW BVH's margin argument).
 struct ObjBvh {
   const std::vector<Bounds> &b;
   const std::vector<double> &w;  // per-object test cost (relative)
-  double margin;
+  const std::vector<double> &m;  // per-object box margin
   std::vector<Node> nodes;
   std::vector<int32_t> order;
 
@@ -363,18 +363,21 @@ struct ObjBvh {
     const int me = int(nodes.size());
     nodes.push_back(Node{});
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    double glo[3] = {INFINITY, INFINITY, INFINITY}, ghi[3] = {-INFINITY, -INFINITY, -INFINITY};
     double wsum = 0;
     for (int i = 0; i < cnt; ++i) {
       wsum += w[ids[i]];
       for (int a = 0; a < 3; ++a) {
         lo[a] = std::min(lo[a], b[ids[i]].lo[a]);
         hi[a] = std::max(hi[a], b[ids[i]].hi[a]);
+        glo[a] = std::min(glo[a], b[ids[i]].lo[a] - m[ids[i]]);
+        ghi[a] = std::max(ghi[a], b[ids[i]].hi[a] + m[ids[i]]);
       }
     }
     Node nd{};
-    for (int a = 0; a < 3; ++a) {
-      nd.bmin[a] = std::nextafter(float(lo[a] - margin), -INFINITY);
-      nd.bmax[a] = std::nextafter(float(hi[a] + margin), INFINITY);
+    for (int a = 0; a < 3; ++a) {  // every object grown by its own margin
+      nd.bmin[a] = std::nextafter(float(glo[a]), -INFINITY);
+      nd.bmax[a] = std::nextafter(float(ghi[a]), INFINITY);
     }
     // best SAH split: cost = C_trav * A + A_L * W_L + A_R * W_R (A = area)
     const double pa = std::max(area(lo, hi), 1e-30);
@@ -473,7 +476,19 @@ int build_device_scene(rt_nw_scene *s, DeviceScene &out) {
     const Obj &o = s->flat_obj[k];
     cost[k] = (o.kind == kBox ? 3.0 : o.kind == kMovingSphere ? 1.2 : 1.0) + (o.inst >= 0 ? 0.3 : 0.0);
   }
-  ObjBvh bvh{s->flat_bounds, cost, 1e-3 * (1.0 + scale), {}, {}};
+  // box margins (the RTIOW BVH's argument): 1e-3 of the
+  // object's own coordinate scale — ~100x the float error of its hit test —
+  // plus 1e-6 of the scene's, for rays from far away.  One scene-wide margin
+  // of 1e-3 of the scene scale grew every small box by ~2 units next to the
+  // R = 1000 ground (137 node visits per camera ray instead of ~20).
+  std::vector<double> margin(n_all, 0.0);
+  for (int32_t k : ids) {
+    double own = 0;
+    for (int a = 0; a < 3; ++a)
+      own = std::max(own, std::max(std::fabs(s->flat_bounds[k].lo[a]), std::fabs(s->flat_bounds[k].hi[a])));
+    margin[k] = 1e-3 * (1.0 + own) + 1e-6 * scale;
+  }
+  ObjBvh bvh{s->flat_bounds, cost, margin, {}, {}};
   const int n = int(ids.size());
   if (n > 0) bvh.build(ids.data(), n);
   out.nodes = std::move(bvh.nodes);

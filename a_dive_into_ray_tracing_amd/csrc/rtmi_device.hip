@@ -910,10 +910,10 @@ constexpr size_t kBvhLdsMax = 64 * 1024;  // BVH bytes staged per block (DESIGN.
 // BVH over the small spheres: binary, SAH split (full sweep of the sorted
 // centroids on each axis: the split minimising area(L)*|L| + area(R)*|R|),
 // leaves of <= kLeafMax spheres, nodes in DFS order with skip links.  Boxes
-// are the spheres' double-precision bounds grown by a margin (1e-3 of the
-// scene scale, ~100x the float error of the sphere test at that scale) and
-// rounded outward to half precision, so every sphere the float test can
-// report lies strictly inside its leaf's box.
+// are the spheres' double-precision bounds, each grown by its own margin (1e-3
+// of the sphere's coordinate scale, ~100x the float error of its hit test,
+// plus 1e-6 of the scene's) and rounded outward to half precision, so every
+// sphere the float test can report lies strictly inside its leaf's box.
 uint16_t half_bits(_Float16 h) { return __builtin_bit_cast(uint16_t, h); }
 // largest half <= v (-inf below the half range)
 uint16_t half_down(double v) {
@@ -932,7 +932,7 @@ uint16_t half_up(double v) { return uint16_t(half_down(-v) ^ 0x8000); }
 struct BvhBuilder {
   const double *cr;
   const std::vector<float4> &g;
-  double margin;
+  double margin_scene;  // 1e-6 of the whole scene's scale (rays from far away)
   std::vector<BvhNode> nodes;
   std::vector<float4> sph;
   std::vector<int32_t> idx;
@@ -950,9 +950,16 @@ struct BvhBuilder {
       return e0 * e1 + e1 * e2 + e0 * e2;
     }
   };
+  // sphere k's box margin: 1e-3 of its own coordinate scale (~100x the float
+  // error of its hit test) + margin_scene
+  double margin(int32_t k) const {
+    const double *c = cr + 4 * k;
+    const double own = std::max(std::max(std::fabs(c[0]), std::fabs(c[1])), std::fabs(c[2])) + std::fabs(c[3]);
+    return 1e-3 * (1.0 + own) + margin_scene;
+  }
   Box bounds(const int32_t *ids, int cnt) const {
     Box b;
-    for (int i = 0; i < cnt; ++i) b.add(cr + 4 * ids[i], std::fabs(cr[4 * ids[i] + 3]) + margin);
+    for (int i = 0; i < cnt; ++i) b.add(cr + 4 * ids[i], std::fabs(cr[4 * ids[i] + 3]) + margin(ids[i]));
     return b;
   }
   void sort_axis(int32_t *ids, int cnt, int ax) const {
@@ -984,12 +991,12 @@ struct BvhBuilder {
         sort_axis(ids, cnt, ax);
         Box l;
         for (int i = 1; i < cnt; ++i) {
-          l.add(cr + 4 * ids[i - 1], std::fabs(cr[4 * ids[i - 1] + 3]) + margin);
+          l.add(cr + 4 * ids[i - 1], std::fabs(cr[4 * ids[i - 1] + 3]) + margin(ids[i - 1]));
           left_cost[i] = l.area() * i;
         }
         Box r;
         for (int i = cnt - 1; i >= 1; --i) {
-          r.add(cr + 4 * ids[i], std::fabs(cr[4 * ids[i] + 3]) + margin);
+          r.add(cr + 4 * ids[i], std::fabs(cr[4 * ids[i] + 3]) + margin(ids[i]));
           const double c = left_cost[i] + r.area() * (cnt - i);
           if (c < best) { best = c; best_ax = ax; best_mid = i; }
         }
@@ -1087,13 +1094,12 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
     std::nth_element(sorted_r.begin(), sorted_r.begin() + n / 2, sorted_r.end());
     const double med = sorted_r[n / 2];
     std::vector<int32_t> big, small;
-    double scale = 0;
+    double scale = 0;  // the whole scene's, big spheres included
     for (int k = 0; k < n; k++) {
       (rad[k] > RTMI_BIG_FACTOR * med ? big : small).push_back(k);
-      if (rad[k] <= RTMI_BIG_FACTOR * med)
-        for (int a = 0; a < 3; ++a) scale = std::max(scale, std::fabs(scene->center_radius[4 * k + a]) + rad[k]);
+      for (int a = 0; a < 3; ++a) scale = std::max(scale, std::fabs(scene->center_radius[4 * k + a]) + rad[k]);
     }
-    BvhBuilder b{scene->center_radius, g, 1e-3 * (1.0 + scale), {}, {}, {}};
+    BvhBuilder b{scene->center_radius, g, 1e-6 * scale, {}, {}, {}};
     if (!small.empty()) b.build(small.data(), int(small.size()));
     const int nb_pad = big.empty() ? 0 : (int(big.size()) + 2 * kBigGroup - 1) / (2 * kBigGroup) * (2 * kBigGroup);
     std::vector<SpherePair> bp(nb_pad / 2 + kPairGroup);

@@ -155,10 +155,19 @@ def device_count():
     return n.value if rc == 0 else 0
 
 
+def auto_tile_w(W, rows):
+    """The tile width `rt_render_rows` picks when tile_w is 0 (rtmi_device.hip
+    auto_tile_w): 8 unless 16x4 tiles leave fewer idle lanes in partial tiles."""
+    def idle(tw):
+        th = 64 // tw
+        return -(-W // tw) * tw * (-(-rows // th)) * th - W * rows
+    return 16 if idle(16) < idle(8) else 8
+
+
 class Renderer:
     """One rt_ctx: a device, its stream and the resident scene."""
 
-    def __init__(self, world, device=0, tile_w=8, chunk=0):
+    def __init__(self, world, device=0, tile_w=0, chunk=0):
         self.L = load()
         self._h = C.c_void_p()
         check(self.L.rt_ctx_create(device, C.byref(self._h)), "rt_ctx_create")
@@ -171,7 +180,7 @@ class Renderer:
         check(self.L.rt_ctx_set_scene(self._h, C.byref(sc)), "rt_ctx_set_scene")
         self.world = world
 
-    def set_tuning(self, tile_w=8, chunk=0):
+    def set_tuning(self, tile_w=0, chunk=0):
         check(self.L.rt_ctx_set_tuning(self._h, tile_w, chunk), "rt_ctx_set_tuning")
 
     def set_schedule(self, chunk=0, tail_spp=-1, tail_chunk=0):

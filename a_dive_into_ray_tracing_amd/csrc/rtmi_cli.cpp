@@ -5,7 +5,7 @@
 //
 //   rtmi_render [--scene final|learn] [--width W] [--height H] [--spp S]
 //               [--depth D] [--seed N] [--gpus G] [--out FILE|-] [--p6]
-//               [--tile-w 8|16|32|64] [--chunk N] [--scene-file F]
+//               [--tile-w 0|8|16|32|64] [--chunk N] [--scene-file F]
 //               [--save-scene F] [--pfm F] [--pass-spp N [--checkpoint F]]
 //
 // --gpus 1 uses rt_render on device 0; --gpus G>1 (or 0 = all) uses
@@ -35,7 +35,7 @@ static int die(const char *what, int rc) {
 
 int main(int argc, char **argv) {
   std::string scene = "final", out = "-", scene_file, save_scene, pfm, checkpoint;
-  int W = 1200, H = -1, spp = 500, depth = 50, gpus = 1, p6 = 0, tile_w = 8, chunk = 0, pass_spp = 0;
+  int W = 1200, H = -1, spp = 500, depth = 50, gpus = 1, p6 = 0, tile_w = 0, chunk = 0, pass_spp = 0;
   unsigned long long seed = 1984;
   for (int a = 1; a < argc; a++) {
     auto need = [&](const char *f) -> const char * {

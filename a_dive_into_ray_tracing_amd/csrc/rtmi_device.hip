@@ -64,6 +64,11 @@ struct RenderArgs {
   // block's waves, no phase 2), so the block sums its waves' accumulators and
   // flushes once (a quarter of the global atomics)
   int32_t block_flush;
+  // block_flush launches only: the block's waves draw (pixel, sample) jobs
+  // from ONE pool covering their 4 items (an LDS counter), so they drain
+  // together instead of each wave ramping down alone (same image: the
+  // accumulators are fixed point, their sums independent of who adds)
+  int32_t block_pool;
   // progressive passes: this launch renders samples s_base + [0, spp)
   int32_t s_base;
   uint64_t out_elems;  // elements of accum / out (RTMI_CHECK builds verify every write)
@@ -159,10 +164,14 @@ __global__ __launch_bounds__(64 * GridShape<BVH>::waves, GridShape<BVH>::per_eu)
   constexpr int WPB = GridShape<BVH>::waves;
   __shared__ unsigned long long acc[WPB][3][64];
   __shared__ unsigned long long wave_segs[WPB];
+  __shared__ unsigned pool_next;  // block pool: next unclaimed job
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * WPB + wave;
+  const bool pool = CHUNKED && a.block_pool;  // block-uniform (implies block_flush)
+  if (pool && threadIdx.x == 0) pool_next = 64 * WPB;
   if constexpr (BVH) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
+  else if (pool) __syncthreads();
   if (item >= a.n_items) return;  // wave-uniform; no block barrier follows
 
   int tile, s0, ns;
@@ -181,7 +190,17 @@ __global__ __launch_bounds__(64 * GridShape<BVH>::waves, GridShape<BVH>::per_eu)
   const int x0 = tx * TW, y0 = ty * TH;
   const int vw = min(TW, a.W - x0), vh = min(TH, a.nrows_valid - y0);
   const int nv = vw * vh;  // valid pixels of this tile
-  const int nq = nv * ns;  // jobs: (pixel, sample) pairs of this item
+  int nq = nv * ns;  // jobs: (pixel, sample) pairs of this item
+  int q0 = lane;     // this lane's first job
+  if (pool) {
+    // the block's WPB items are consecutive sample ranges of one tile
+    // (block_flush schedule): one job range [s0 of the first item, its end)
+    const int sb0 = (int(blockIdx.x) * WPB % a.nch1) * a.chunk1;
+    const int sb1 = min(sb0 + WPB * a.chunk1, a.spp1);
+    s0 = sb0;
+    nq = nv * max(sb1 - sb0, 0);
+    q0 = wave * 64 + lane;
+  }
 
   acc[wave][0][lane] = 0;
   acc[wave][1][lane] = 0;
@@ -218,8 +237,8 @@ __global__ __launch_bounds__(64 * GridShape<BVH>::waves, GridShape<BVH>::per_eu)
     depth = 0;
   };
 
-  bool active = lane < nq;
-  if (active) start(lane);
+  bool active = q0 < nq;
+  if (active) start(q0);
   int next = 64;
 
   for (;;) {
@@ -281,6 +300,11 @@ __global__ __launch_bounds__(64 * GridShape<BVH>::waves, GridShape<BVH>::per_eu)
     }
     const unsigned long long m = __ballot(done);
     if (m) {
+      if (pool) {  // claim popcount(m) jobs of the block pool (one LDS atomic)
+        unsigned b = 0;
+        if (lane == 0) b = atomicAdd(&pool_next, unsigned(__popcll(m)));
+        next = __builtin_amdgcn_readlane(int(b), 0);
+      }
       if (done) {
         atomicAdd(&acc[wave][0][px], (unsigned long long)to_fixed(col.x));
         atomicAdd(&acc[wave][1][px], (unsigned long long)to_fixed(col.y));
@@ -782,6 +806,8 @@ struct rt_ctx {
   // block-level accumulator flush of the automatic grid schedule (same image;
   // RTMI_BLOCK_FLUSH=0 in the environment turns it off, for A/B and tests)
   bool block_flush = !(std::getenv("RTMI_BLOCK_FLUSH") && std::getenv("RTMI_BLOCK_FLUSH")[0] == '0');
+  // block-shared job pool of block_flush launches (same image; RTMI_BLOCK_POOL=0 turns it off)
+  bool block_pool = !(std::getenv("RTMI_BLOCK_POOL") && std::getenv("RTMI_BLOCK_POOL")[0] == '0');
   unsigned *cost_prev = nullptr, *cost_cur = nullptr, *cost_sorted = nullptr;
   int32_t *order = nullptr, *iota = nullptr;
   size_t cost_cap = 0;  // tiles
@@ -791,7 +817,7 @@ struct rt_ctx {
   int64_t cost_key[6] = {0, 0, 0, 0, 0, 0};  // W, H, row0, row_step, nvalid, tile_w
   hipStream_t last_stream = nullptr;
   hipEvent_t last_done = nullptr;  // end of the last render's work on last_stream
-  int32_t tile_w = 8;
+  int32_t tile_w = 0;  // 0 = automatic per launch (auto_tile_w)
   int32_t chunk = 0;       // phase-1 samples per item (0 = automatic)
   int32_t tail_spp = -1;   // samples in the short-item phase (-1 = automatic)
   int32_t tail_chunk = 0;  // phase-2 samples per item (0 = automatic)
@@ -1161,10 +1187,22 @@ RTMI_EXPORT int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind) {
   return RT_OK;
 }
 
+// Automatic tile shape: 8x8 unless 16x4 leaves fewer idle lanes in partial
+// tiles.  A 100-row strip (1/8 of config 2's rows) fills 25 rows of 16x4 tiles
+// but 12.5 of 8x8: 7.04 vs 7.16 ms, while the whole frame runs 50.6 ms with 8x8
+// and 50.9 with 16x4 (profiles/r01/session6/tile_ab.txt).
+static int auto_tile_w(int32_t W, int32_t rows) {
+  auto idle = [&](int64_t tw) {
+    const int64_t th = 64 / tw;
+    return ((W + tw - 1) / tw) * tw * ((rows + th - 1) / th) * th - int64_t(W) * rows;
+  };
+  return idle(16) < idle(8) ? 16 : 8;
+}
+
 RTMI_EXPORT int rt_ctx_set_tuning(rt_ctx *ctx, int32_t tile_w, int32_t chunk) {
   if (!ctx) return set_error(RT_EINVAL, "null ctx");
-  if (tile_w != 8 && tile_w != 16 && tile_w != 32 && tile_w != 64)
-    return set_error(RT_EINVAL, "tile_w must be 8, 16, 32 or 64");
+  if (tile_w != 0 && tile_w != 8 && tile_w != 16 && tile_w != 32 && tile_w != 64)
+    return set_error(RT_EINVAL, "tile_w must be 0 (automatic), 8, 16, 32 or 64");
   if (chunk < 0) return set_error(RT_EINVAL, "chunk must be >= 0");
   ctx->tile_w = tile_w;
   ctx->chunk = chunk;
@@ -1237,7 +1275,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     if (!pass_accum) HIP_TRY(hipMemsetAsync(strip, 0, size_t(nvalid) * W * 3 * sizeof(float), st));
     return RT_OK;
   }
-  const int TW = ctx->tile_w, TH = 64 / TW;
+  const int TW = ctx->tile_w ? ctx->tile_w : auto_tile_w(W, nvalid), TH = 64 / TW;
   const int tiles_x = (W + TW - 1) / TW;
   const int tiles_y = (nvalid + TH - 1) / TH;
   const int64_t tiles = int64_t(tiles_x) * tiles_y;
@@ -1262,10 +1300,14 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     const int64_t waves = int64_t(ctx->resident_blocks) * kWavesPerBlock;
     chunk1 = int32_t(std::min<int64_t>(64, std::max<int64_t>(4, tile_samples / (28 * waves))));
   } else if (chunk1 <= 0) {
-    // at least 24 samples per item: a 1/8 strip of config 2 (BVH, cost order)
-    // runs 7.58 ms with 16, 7.39 with 24, 7.48 with 32 (profiles/r01/session2)
-    const int64_t want_items = 150000;
-    chunk1 = int32_t(std::min<int64_t>(64, std::max<int64_t>(24, tile_samples / want_items)));
+    // ~60 k items of 24..125 samples (BVH, cost order, block flush; the
+    // rounding below keeps a multiple of 4 items per tile): config 2 runs
+    // 52.5 ms with chunk 21, 51.1 with 42, 50.8 with 63, 50.7 with 125; one
+    // rank's 1/8 strip 8.06 ms with 7, 7.37 with 14, 7.18 with 21, 7.27 with
+    // 32 (profiles/r01/session6/chunk_ab.txt): long items pay the per-item
+    // ramp-down less often, short ones shorten a small grid's dispatch tail
+    const int64_t want_items = 60000;
+    chunk1 = int32_t(std::min<int64_t>(125, std::max<int64_t>(24, tile_samples / want_items)));
   }
   if (chunk2 <= 0) chunk2 = std::max(1, chunk1 / 4);
   if (tail < 0) tail = 0;  // automatic: no short-item phase (it measured no better)
@@ -1294,6 +1336,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   a.tiles_x = tiles_x; a.n_items = int32_t(items);
   a.tiles = int32_t(tiles); a.spp1 = spp1; a.chunk1 = chunk1; a.nch1 = nch1; a.chunk2 = chunk2; a.nch2 = nch2;
   a.block_flush = !persistent && nch2 == 0 && nch1 % grid_wpb == 0 && ctx->block_flush;
+  a.block_pool = a.block_flush && ctx->block_pool;
   a.s_base = s_base;
   a.out_elems = uint64_t(nvalid) * uint64_t(W) * 3;
   const bool chunked = pass_accum || nch1 + nch2 > 1;

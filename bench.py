@@ -121,7 +121,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--tile-w", type=int, default=8)
+    ap.add_argument("--tile-w", type=int, default=0, help="0 = automatic (the library default)")
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--tail-spp", type=int, default=-1)
     ap.add_argument("--tail-chunk", type=int, default=0)
@@ -161,6 +161,7 @@ def main():
     if args.strip_of > 1 and N == 1:  # analysis mode: one rank's share of an N-GPU render
         row0, row_step, nrows = rdist.strip_rows(H, 0, args.strip_of)
     strip = torch.empty((nrows, W, 3), dtype=torch.float32, device=dev)
+    tw = args.tile_w or rt.auto_tile_w(W, -(-(H - row0) // row_step) if row0 < H else 0)  # reported tile shape
     gathered = None
     # a non-default stream: the kernel, its HIP events and the RCCL gather
     # are all ordered on it (the null stream would bypass the events)
@@ -261,7 +262,7 @@ def main():
                 "workload": f"rtiow_final_{W}x{H}_{SPP}spp_depth{DEPTH}",
                 "width": W, "height": H, "spp": SPP, "max_depth": DEPTH, "seed": SEED, "spheres": len(world),
                 "partition": "interleaved rows, one RCCL gather" if N > 1 else "single GPU",
-                "tile": f"{args.tile_w}x{64 // args.tile_w}",
+                "tile": f"{tw}x{64 // tw}" + ("" if args.tile_w else " (auto)"),
                 "kernel": args.kernel,
                 "accel": args.accel,
                 "ordering": args.ordering,

@@ -122,8 +122,9 @@ int rt_ctx_destroy(rt_ctx *ctx);
 /* Upload the scene (replaces the per-thread copies of `world`,
  * main.cpp:331-333).  Synchronous; O(n). */
 int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene);
-/* Tuning: tile_w in {8, 16, 32, 64} (tile = tile_w x 64/tile_w pixels per
- * wavefront); chunk = samples per work item (0 = automatic).  Neither
+/* Tuning: tile_w in {0, 8, 16, 32, 64} (tile = tile_w x 64/tile_w pixels per
+ * wavefront; 0 = automatic, the default: 8 unless 16 leaves fewer idle lanes
+ * in partial tiles); chunk = samples per work item (0 = automatic).  Neither
  * changes the image. */
 int rt_ctx_set_tuning(rt_ctx *ctx, int32_t tile_w, int32_t chunk);
 /* Work schedule: the first spp - tail_spp samples of every tile in items of

@@ -32,3 +32,16 @@ def test_flop_kinds_cover_the_object_kinds():
     # every non-medium kind of rtmi_nw_types.h ObjKind has a cost
     assert sorted(bench.NW_FLOP) == [0, 1, 2, 3, 4, 5]
     assert all(v > 0 for v in bench.NW_FLOP.values())
+
+
+def test_auto_tile_w_rule():
+    """The automatic tile shape (rtmi_device.hip auto_tile_w, mirrored by
+    rt.auto_tile_w for reporting): 8x8 unless 16x4 leaves fewer idle lanes."""
+    import a_dive_into_ray_tracing_amd as rt
+
+    assert rt.auto_tile_w(1200, 800) == 8  # whole frame: both fill every tile
+    assert rt.auto_tile_w(1200, 100) == 16  # 1/8 strip: 12.5 rows of 8x8 tiles, 25 of 16x4
+    assert rt.auto_tile_w(1200, 400) == 8 and rt.auto_tile_w(1200, 200) == 8
+    assert rt.auto_tile_w(3840, 270) == 8  # 1/8 of 2160 rows: 270 = 4 * 67 + 2, no shape fills it
+    assert rt.auto_tile_w(1204, 8) == 8  # columns: 8 wastes 4 per row of tiles, 16 wastes 12
+    assert rt.auto_tile_w(29, 19) in (8, 16)

@@ -98,7 +98,7 @@ def test_exact_replay_reproduces_reference_image(name, W, H, S, final_renderer, 
 
 # ------------------------------------------------------------ tier 2 -------
 @pytest.mark.parametrize("kernel", ["persistent", "grid"])
-@pytest.mark.parametrize("tile_w", [8, 16, 32, 64])
+@pytest.mark.parametrize("tile_w", [0, 8, 16, 32, 64])
 @pytest.mark.parametrize("chunk", [0, 3, 1000])
 def test_fast_kernel_bit_exact_vs_oracle_final(kernel, tile_w, chunk, final_world, final_renderer):
     W, H, S = 48, 32, 8
@@ -108,7 +108,7 @@ def test_fast_kernel_bit_exact_vs_oracle_final(kernel, tile_w, chunk, final_worl
     try:
         got = final_renderer.render(cam, W, H, S, 50, SEED)
     finally:
-        final_renderer.set_tuning(8, 0)
+        final_renderer.set_tuning(0, 0)
         final_renderer.set_kernel("auto")
     want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
     assert np.array_equal(got, want), np.abs(got - want).max()
@@ -414,22 +414,29 @@ def test_cost_ordered_dispatch_same_image(kernel, accel, final_world, final_rend
 
 
 @pytest.mark.parametrize("accel", ["none", "bvh"])
-def test_block_flush_same_image(accel, final_world, monkeypatch):
+@pytest.mark.parametrize("W,H,S", [(40, 24, 37), (29, 19, 5)])
+def test_block_flush_same_image(accel, W, H, S, final_world, monkeypatch):
     """The automatic grid schedule gives every block the items of one tile and
-    flushes the block's summed accumulators once; RTMI_BLOCK_FLUSH=0 flushes
-    per wave.  Same image bit for bit, and equal to the oracle."""
-    W, H, S = 40, 24, 37  # 37 spp: 4 items of 10/10/10/7 samples per tile
+    flushes the block's summed accumulators once; its waves draw their
+    (pixel, sample) jobs from one block-wide pool.  RTMI_BLOCK_POOL=0 keeps a
+    pool per wave, RTMI_BLOCK_FLUSH=0 also flushes per wave.  Same image and
+    world.hit count bit for bit, equal to the oracle.  37 spp: 4 items of
+    10/10/10/7 samples per tile; 29x19 at 5 spp: partial tiles, items of
+    2/2/1/0 samples (a wave with an empty item still draws from the pool)."""
     cam = rt.final_camera(W / H)
-    imgs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("RTMI_BLOCK_FLUSH", flag)
+    imgs, segs = [], []
+    for flush, pool in (("1", "1"), ("1", "0"), ("0", "1")):
+        monkeypatch.setenv("RTMI_BLOCK_FLUSH", flush)
+        monkeypatch.setenv("RTMI_BLOCK_POOL", pool)
         r = rt.Renderer(final_world, 0)
         try:
             r.set_kernel("grid")
             r.set_accel(accel)
             imgs.append(r.render(cam, W, H, S, 50, SEED))
+            segs.append(r.last_segments())
         finally:
             r.close()
-    assert np.array_equal(imgs[0], imgs[1])
+    assert np.array_equal(imgs[0], imgs[1]) and np.array_equal(imgs[0], imgs[2])
+    assert segs[0] == segs[1] == segs[2]
     want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
     assert np.array_equal(imgs[0], want)

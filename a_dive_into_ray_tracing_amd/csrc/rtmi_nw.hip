@@ -11,6 +11,7 @@
 // Per path segment: stackless BVH walk over the flattened objects (the
 // reference walks a pointer tree of virtual hittables), deferred hit record
 // of the winner, then texture lookup and scatter.
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -523,7 +524,19 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
   a.nrows_valid = valid;
   a.tiles_x = (W + 7) / 8;
   a.tiles = a.tiles_x * ((valid + 7) / 8);
-  a.chunk = std::min(spp, 32);
+  // samples per work item (same image for any size; RTMI_NW_CHUNK overrides,
+  // for A/B).  Automatic: ~80 items per resident wave of the persistent
+  // kernel, 4..32 samples: the final scene (fog, lights: long and uneven paths)
+  // at 256 spp runs 329 ms with 8, 433 with 32; at 1024 spp 1215 ms with 24,
+  // 1205 with 32, 1308 with 8 — the item count, not the size, sets its tail
+  // (profiles/r01/session6/nw_chunk.txt)
+  static const int env_chunk = std::getenv("RTMI_NW_CHUNK") ? std::atoi(std::getenv("RTMI_NW_CHUNK")) : 0;
+  int64_t chunk = 32;
+  if (ctx->persist_blocks > 0) {
+    const int64_t waves = int64_t(ctx->persist_blocks) * kPWaves;
+    chunk = std::min<int64_t>(32, std::max<int64_t>(4, int64_t(a.tiles) * spp / (80 * waves)));
+  }
+  a.chunk = std::min<int64_t>(spp, env_chunk > 0 ? env_chunk : chunk);
   a.nch = (spp + a.chunk - 1) / a.chunk;
   if (int64_t(a.tiles) * a.nch >= (int64_t(1) << 31) - kWaves) return set_error(RT_EINVAL, "render too large");
   a.n_items = a.tiles * a.nch;

@@ -11,22 +11,34 @@ j % N), each rank renders its strip on its own GPU, and the strips are
 gathered to rank 0 with ONE RCCL gather (torch.distributed "nccl" = RCCL)
 inside the timed region.  Total work is fixed as N grows: scaling "strong".
 value = W*H*spp*K / max-over-ranks(wall time of K steps) / 1e6.
+`--gpus N` without a launcher environment starts the N ranks itself (a
+torch.distributed.run child of a parent that never touches the GPU) and
+refuses to run when fewer than N GPUs are visible.  After the timed region
+rank 0 renders the whole frame alone and checks the gathered image against
+it bit for bit ("gather_check").
 
 Closest hits go through the BVH by default (--accel bvh): the same closest
 hit as the brute-force loop, bit for bit (tests/test_gpu_parity.py), so the
 same image.  --accel none times the brute-force kernel.
 
-roofline: FP32 VALU.  achieved = segments * 18 * 487 FLOP per launch
-(SURVEY §8(d): 18 flops per ray-sphere test, brute force over 487 spheres;
-segments = world.hit calls, counted exactly on the GPU) / mean launch time
-from HIP events on the launch stream; peak = 157.3 TFLOP/s FP32 vector.
-With the BVH this is the brute-force-equivalent ("work_equivalent", as
-SURVEY §8(d) prescribes for culling), so frac can exceed 1; roofline.
-brute_force gives the brute-force kernel's own figure from one extra,
-untimed launch of the same rows.
-cpu_baseline: the reference itself (oracle/_ref/ref_harness: worker() at -O2,
-16 std::threads as the reference's concurrency) on a bounded sample, rank 0,
-N = 1 only.
+roofline (FP32 VALU): `achieved` = the EXECUTED algorithmic FLOP
+of the timed kernel's launch / its mean duration (HIP events on the launch
+stream).  With the BVH the executed work is counted exactly by the
+RTMI_STATS build of the same kernel (librtmi_stats.so, one extra untimed
+render of the same rows in a child process; same paths, same image):
+every lane's node slab tests x 25 FLOP (6 FMA + 12 min/max + 1 compare) plus
+its sphere miss tests (leaf spheres and the brute-force big spheres) x 18
+FLOP (sphere.h:21-55).  Brute force executes segments x N x 18.
+peak = 157.3 TFLOP/s FP32 vector.  `work_equivalent_*` keeps SURVEY §8(d)'s
+brute-force-equivalent figure (segments x 487 x 18 over the BVH time, which
+can exceed 1) and `brute_force_*` the brute-force kernel's own roofline from
+one more untimed launch of the same rows.
+cpu_baseline (BASELINE.md §4, rank 0, N = 1): host facts (CPU model, sockets,
+cores per socket, the CPU share this job may load), every run pinned with
+taskset to one physical core per thread on one socket: (ii) the reference's
+worker() at -O2 with threads = the CPU share (the reported value), (i) the as-shipped -O0 build with
+the reference's 16 threads, (iii) this build's C restatement (fast mode,
+OpenMP) at -O3 -march=native — each on a bounded sample.
 
 --workload config4 / config5 time BASELINE's other final-scene configs
 (1200x800 at 5000 spp; 3840x2160 at 2000 spp).  It also selects the
@@ -39,6 +51,7 @@ default 1024).  Same row partition and gather as the headline.
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -49,7 +62,8 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 W, H, SPP, DEPTH, SEED = 1200, 800, 500, 50, 1984
-FLOP_PER_SPHERE_TEST = 18
+FLOP_PER_SPHERE_TEST = 18  # oc 3, hb 5, |oc|^2-r^2 7, disc 3
+FLOP_PER_NODE_TEST = 25  # slab test as executed: 6 FMA (12) + 12 min/max + 1 compare
 PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector (MI355X_MICROARCH.md)
 PUBLISHED_CPU_MSPS = 0.1189  # README.md:16-19: rt_in_one_weekend, 1200x800x500, 16 threads, 4036.1 s
 METRIC = "Msamples/sec (pixels x spp) on RTIOW final scene"
@@ -58,6 +72,44 @@ METRIC = "Msamples/sec (pixels x spp) on RTIOW final scene"
 # camera) at 2000 spp (quoted for 8 GPUs; the final scene has the
 # reference's defocus blur, aperture 0.1).
 RTIOW_WORKLOADS = {"config2": (1200, 800, 500), "config4": (1200, 800, 5000), "config5": (3840, 2160, 2000)}
+STATS_LIB = os.path.join(REPO, "a_dive_into_ray_tracing_amd", "lib", "librtmi_stats.so")
+
+
+# ----------------------------------------------------------------- launch ----
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(gpus, argv, port):
+    """The torch.distributed.run command that starts `gpus` ranks of this
+    script with the same arguments (one process per GPU)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def visible_gpus():
+    """GPUs this process could use, counted without initialising the GPU
+    (torch.cuda.device_count() does not create a context on this image)."""
+    import torch
+
+    return torch.cuda.device_count()
+
+
+def launch(args, argv):
+    """--gpus N > 1 without a launcher environment: check that N GPUs are
+    visible, then run N ranks as a torch.distributed.run child and exit with
+    its status.  This process never touches the GPU (no exec after GPU init)."""
+    backend = os.environ.get("RTMI_DIST_BACKEND", "nccl")
+    n = visible_gpus()
+    if backend == "nccl" and n < args.gpus:
+        print(f"bench: {args.gpus} GPUs asked, {n} visible — refusing to report a {n}-GPU run as {args.gpus}",
+              file=sys.stderr, flush=True)
+        return 2
+    cmd = launch_command(args.gpus, argv, free_port())
+    print(f"bench: launching {args.gpus} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
 
 
 def dist_setup(torch, dist):
@@ -70,7 +122,10 @@ def dist_setup(torch, dist):
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("RTMI_DIST_BACKEND", "nccl")
-    device = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and local_rank >= ndev:
+        raise SystemExit(f"bench: rank {rank} needs GPU {local_rank}, {ndev} visible")
+    device = local_rank % max(1, ndev) if backend == "gloo" else local_rank
     torch.cuda.set_device(device)
     dev = torch.device("cuda", device)
     if world_size > 1:
@@ -82,41 +137,186 @@ def dist_setup(torch, dist):
     return world_size, rank, device, dev, coll
 
 
-def cpu_baseline(threads=16):
-    """The reference's own worker() (oracle/_ref/ref_harness bench) on a
-    bounded sample: full 1200x800 image at 4 spp (~3.8 M samples)."""
-    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
-    spp = 4
-    if os.path.exists(harness):
-        try:
-            out = subprocess.run([harness, "bench", str(threads), str(W), str(H), str(spp), str(DEPTH)],
-                                 capture_output=True, text=True, timeout=300, check=True).stdout
-            r = json.loads(out.strip().splitlines()[-1])
-            return {"value": round(r["msamples_per_s"], 5), "unit": "Msamples/s", "cores": threads, "kind": "reference",
-                    "sample": f"reference worker() g++ -O2, {threads} std::threads, final scene {W}x{H}x{spp}spp depth {DEPTH} "
-                              f"({r['seconds']:.1f} s wall)"}
-        except Exception as e:  # fall through to the port
-            print(f"bench: reference harness failed: {e}", file=sys.stderr)
+# ------------------------------------------------------- executed work ----
+def executed_counts_child(argv):
+    """--exec-counts child (RTMI_LIBRARY = the RTMI_STATS build): render the
+    given rows once and print the exact per-lane work counters as JSON."""
+    import ctypes as C
+
+    import torch
+
+    import a_dive_into_ray_tracing_amd as rt
+
+    Wc, Hc, S, row0, row_step, nrows = (int(x) for x in argv[:6])
+    accel = argv[6]
+    L = rt.load()
+    L.rt_ctx_debug_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+    L.rt_ctx_debug_counters.restype = C.c_int
+    world = rt.random_scene()
+    r = rt.Renderer(world, 0)
+    r.set_accel(accel)
+    strip = torch.empty((nrows, Wc, 3), dtype=torch.float32, device="cuda:0")
+    r.render_rows(rt.final_camera(Wc / Hc), Wc, Hc, S, DEPTH, SEED, row0, row_step, nrows, strip.data_ptr(), 0)
+    r.synchronize()
+    v = (C.c_uint64 * 8)()
+    rt.check(L.rt_ctx_debug_counters(r._h, v), "rt_ctx_debug_counters")
+    nbig, nnodes = r.accel_info()
+    print(json.dumps({"segments": v[0], "node_visits": v[5], "leaf_sphere_tests": v[6], "node_iterations_wave": v[1],
+                      "leaf_sphere_iterations_wave": v[2], "root_resolutions_wave": v[4], "big_spheres": nbig,
+                      "bvh_nodes": nnodes, "checksum": float(strip.double().sum().item())}), flush=True)
+    r.close()
+
+
+def executed_counts(Wc, Hc, S, row0, row_step, nrows, accel="bvh"):
+    """Run the RTMI_STATS build on the same rows in a child process."""
+    if not os.path.exists(STATS_LIB):
+        return None, f"{STATS_LIB} not built"
+    env = dict(os.environ, RTMI_LIBRARY=STATS_LIB)
     try:
-        sys.path.insert(0, os.path.join(REPO, "tests"))
-        import oracle_py as O
-        import ctypes
+        out = subprocess.run([sys.executable, os.path.abspath(__file__), "--exec-counts", str(Wc), str(Hc), str(S),
+                              str(row0), str(row_step), str(nrows), accel],
+                             capture_output=True, text=True, timeout=240, env=env, check=True).stdout
+        return json.loads(out.strip().splitlines()[-1]), None
+    except Exception as e:  # reported, never replaced by another figure
+        return None, f"stats child failed: {e}"
 
-        sc, _ = O.final_scene()
-        cam = O.final_camera(1.5)
-        rows = 40
-        os.environ.setdefault("OMP_NUM_THREADS", str(threads))
-        t0 = time.perf_counter()
-        O.fast_render(sc, cam, W, H, spp, DEPTH, SEED, row0=0, row_step=H // rows, nrows=rows)
-        dt = time.perf_counter() - t0
-        return {"value": round(rows * W * spp / dt / 1e6, 5), "unit": "Msamples/s", "cores": int(os.environ["OMP_NUM_THREADS"]),
-                "kind": "port", "sample": f"oracle fast-mode C restatement, {rows} rows x {W} x {spp} spp"}
+
+def executed_flop(c):
+    """Executed algorithmic FLOP of one BVH launch from the stats counters."""
+    return (c["node_visits"] * FLOP_PER_NODE_TEST
+            + (c["leaf_sphere_tests"] + c["segments"] * c["big_spheres"]) * FLOP_PER_SPHERE_TEST)
+
+
+# ------------------------------------------------------------ CPU baseline ----
+def host_topology():
+    """(facts, {cpu: (socket, core)}) from lscpu, for the CPUs of this machine."""
+    facts = {"nproc": len(os.sched_getaffinity(0)), "machine_cpus": os.cpu_count()}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=30).stdout
+        keys = {"Model name": "model", "Socket(s)": "sockets", "Core(s) per socket": "cores_per_socket",
+                "Thread(s) per core": "threads_per_core"}
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in keys:
+                v = v.strip()
+                facts[keys[k.strip()]] = int(v) if v.isdigit() else v
+        topo = {}
+        out = subprocess.run(["lscpu", "-p=CPU,CORE,SOCKET"], capture_output=True, text=True, timeout=30).stdout
+        for line in out.splitlines():
+            if line and not line.startswith("#"):
+                cpu, core, sock = (int(x) if x else 0 for x in line.split(","))
+                topo[cpu] = (sock, core)
+    except Exception:
+        topo = {}
+    return facts, topo
+
+
+def socket_cpus(topo, allowed):
+    """The allowed CPUs of one socket (socket 0 when it has any, else the
+    socket with the most), one per physical core first, then SMT siblings."""
+    if not topo:
+        return sorted(allowed)
+    by_sock = {}
+    for c in allowed:
+        by_sock.setdefault(topo.get(c, (0, c))[0], []).append(c)
+    sock = 0 if 0 in by_sock else max(by_sock, key=lambda s: len(by_sock[s]))
+    first, rest, seen = [], [], set()
+    for c in sorted(by_sock[sock]):
+        core = topo.get(c, (0, c))[1]
+        (rest if core in seen else first).append(c)
+        seen.add(core)
+    return first + rest
+
+
+def pinned(cmd, cpus):
+    tp = "/usr/bin/taskset"
+    return ([tp, "-c", ",".join(str(c) for c in cpus)] + cmd) if os.path.exists(tp) else cmd
+
+
+def run_ref_harness(binary, threads, spp, cpus):
+    out = subprocess.run(pinned([binary, "bench", str(threads), str(W), str(H), str(spp), str(DEPTH)], cpus),
+                         capture_output=True, text=True, timeout=300, check=True).stdout
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def cpu_restatement_child(argv):
+    """--cpu-restatement child: the oracle's fast-mode C restatement (OpenMP)
+    on evenly spaced rows of the config-2 image; prints Msamples/s."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_py as O
+
+    rows, spp = int(argv[0]), int(argv[1])
+    sc, _ = O.final_scene()
+    cam = O.final_camera(W / H)
+    t0 = time.perf_counter()
+    O.fast_render(sc, cam, W, H, spp, DEPTH, SEED, row0=0, row_step=H // rows, nrows=rows)
+    dt = time.perf_counter() - t0
+    print(json.dumps({"seconds": dt, "msamples_per_s": rows * W * spp / dt / 1e6, "lib": O.LIB_PATH}), flush=True)
+
+
+def cpu_baseline():
+    """BASELINE.md §4 rows (i)-(iii) on the host of rank 0, pinned to one
+    socket's allowed CPUs.  Reported value: row (ii)."""
+    facts, topo = host_topology()
+    # the CPU share this job may load: OMP_NUM_THREADS where the pool sets it
+    # (16 per GPU on the MI355X boxes), else every allowed CPU
+    share = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
+    cpus = socket_cpus(topo, os.sched_getaffinity(0))[:share]
+    threads = len(cpus)
+    facts["cpu_share"] = share
+    facts["pinned_cpus"] = ",".join(str(c) for c in cpus)
+    facts["pinned_physical_cores"] = len({topo.get(c, (0, c)) for c in cpus}) if topo else None
+    facts["note"] = ("threads = this job's CPU share (OMP_NUM_THREADS), one per physical core of one socket, "
+                     "pinned with taskset; cores_per_socket is the machine's")
+    rows = {}
+    ref = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    ref0 = os.path.join(REPO, "oracle", "_ref", "ref_harness_O0")
+    try:  # (ii) the reference source at -O2, threads = the pinned CPUs
+        spp = 2
+        r = run_ref_harness(ref, threads, spp, cpus)
+        rows["ii_reference_O2"] = {"value": round(r["msamples_per_s"], 5), "threads": threads,
+                                   "sample": f"{W}x{H}x{spp}spp depth {DEPTH}", "seconds": round(r["seconds"], 2)}
     except Exception as e:
-        print(f"bench: cpu baseline unavailable: {e}", file=sys.stderr)
-        return None
+        rows["ii_reference_O2"] = {"error": str(e)[:200]}
+    try:  # (i) as shipped: g++ -O0 (Makefile:7), the reference's 16 threads (main.cpp:318)
+        spp = 1
+        r = run_ref_harness(ref0, 16, spp, cpus)
+        rows["i_as_shipped_O0"] = {"value": round(r["msamples_per_s"], 5), "threads": 16,
+                                   "sample": f"{W}x{H}x{spp}spp depth {DEPTH}", "seconds": round(r["seconds"], 2)}
+    except Exception as e:
+        rows["i_as_shipped_O0"] = {"error": str(e)[:200]}
+    try:  # (iii) this build's CPU restatement, -O3 -march=native, built here
+        import tempfile
+
+        # built on the host it is timed on (never a copy built elsewhere)
+        native = os.path.join(tempfile.mkdtemp(prefix="rtmi_oracle_"), "liboracle_native.so")
+        subprocess.run(["make", "-B", "-C", os.path.join(REPO, "oracle"), "native", f"NATIVE_SO={native}"],
+                       capture_output=True, timeout=120, check=True)
+        env = dict(os.environ, ORACLE_LIBRARY=native, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="true")
+        nrows, spp = 100, 96
+        out = subprocess.run(pinned([sys.executable, os.path.abspath(__file__), "--cpu-restatement", str(nrows), str(spp)], cpus),
+                             capture_output=True, text=True, timeout=300, env=env, check=True).stdout
+        r = json.loads(out.strip().splitlines()[-1])
+        rows["iii_restatement_O3_native"] = {"value": round(r["msamples_per_s"], 5), "threads": threads,
+                                             "sample": f"{nrows} evenly spaced rows x {W} x {spp}spp depth {DEPTH}",
+                                             "seconds": round(r["seconds"], 2)}
+    except Exception as e:
+        rows["iii_restatement_O3_native"] = {"error": str(e)[:200]}
+    main_row = rows["ii_reference_O2"]
+    if "value" not in main_row:
+        return {"value": None, "unit": "Msamples/s", "cores": threads, "kind": "reference", "host": facts, "rows": rows}
+    return {"value": main_row["value"], "unit": "Msamples/s", "cores": threads, "kind": "reference",
+            "sample": f"reference worker() g++ -O2 (oracle/_ref/ref_harness), {threads} std::threads pinned to one "
+                      f"socket, final scene {main_row['sample']} ({main_row['seconds']} s wall)",
+            "host": facts, "rows": rows}
 
 
+# -------------------------------------------------------------------- main ----
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--exec-counts":
+        return executed_counts_child(sys.argv[2:])
+    if len(sys.argv) > 1 and sys.argv[1] == "--cpu-restatement":
+        return cpu_restatement_child(sys.argv[2:])
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -130,11 +330,19 @@ def main():
                     help="closest-hit search: bvh (default; same image bit for bit) or brute force")
     ap.add_argument("--ordering", choices=["cost", "none"], default="cost")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-exec-counts", action="store_true", help="skip the RTMI_STATS work count (roofline.frac null)")
     ap.add_argument("--workload", choices=list(RTIOW_WORKLOADS) + ["nw_motion_blur", "nw_final"], default="config2")
     ap.add_argument("--nw-spp", type=int, default=0, help="spp of the nw_* workloads (default: 500 / 1024)")
     ap.add_argument("--strip-of", type=int, default=0,
                     help="analysis only: time ONE rank's interleaved strip of an N-GPU run on this GPU")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args, sys.argv[1:]))
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws != args.gpus:
+        sys.exit(f"bench: --gpus {args.gpus} but the launcher started {ws} ranks")
     if args.workload.startswith("nw_"):
         return bench_nw(args)
     W, H, SPP = RTIOW_WORKLOADS[args.workload]
@@ -146,8 +354,6 @@ def main():
     from a_dive_into_ray_tracing_amd import dist as rdist
 
     world_size, rank, local_rank, dev, coll = dist_setup(torch, dist)
-    if world_size != args.gpus:
-        print(f"bench: --gpus {args.gpus} but WORLD_SIZE {world_size}", file=sys.stderr)
     N = world_size
 
     world = rt.random_scene()
@@ -170,15 +376,19 @@ def main():
 
     ev = []
 
+    def timed_render(rows=(row0, row_step, nrows), buf=strip):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        r.render_rows(cam, W, H, SPP, DEPTH, SEED, *rows, buf.data_ptr(), stream.cuda_stream)
+        e1.record(stream)
+        return e0, e1
+
     def step(record):
-        if record:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
         nonlocal gathered
-        r.render_rows(cam, W, H, SPP, DEPTH, SEED, row0, row_step, nrows, strip.data_ptr(), stream.cuda_stream)
         if record:
-            e1.record(stream)
-            ev.append((e0, e1))
+            ev.append(timed_render())
+        else:
+            r.render_rows(cam, W, H, SPP, DEPTH, SEED, row0, row_step, nrows, strip.data_ptr(), stream.cuda_stream)
         if N > 1:  # the single exchange step: strips -> rank 0 over RCCL/xGMI
             gathered = rdist.gather_strips(strip if coll.type == "cuda" else strip.cpu(), rank, N, dst=0)
 
@@ -213,38 +423,106 @@ def main():
     else:
         total_segs, kernel_ms_max = float(segs), kernel_ms
 
-    # The brute-force kernel's own VALU roofline, beside the BVH's
-    # work-equivalent one: one more launch of the same rows, untimed.
+    # --- everything below is outside the timed region ---------------------
+    # config-3 parity: the gathered N-GPU image == rank 0's own render of the
+    # whole frame, bit for bit (every pixel's stream is keyed by its
+    # coordinates, so the partition must not change a single value)
+    gather_check = None
+    if N > 1:
+        if rank == 0:
+            full = torch.empty((H, W, 3), dtype=torch.float32, device=dev)
+            e0, e1 = timed_render((0, 1, H), full)
+            torch.cuda.synchronize(dev)
+            img = rdist.unpermute([g.cpu().numpy() for g in gathered], H)
+            ref = full.cpu().numpy()
+            equal = bool(np.array_equal(img, ref))
+            gather_check = {"rows": H, "bit_exact_vs_1gpu_frame": equal, "max_abs_diff": float(np.abs(img - ref).max()),
+                            "one_gpu_frame_ms": round(e0.elapsed_time(e1), 3)}
+            if not equal:
+                print(f"bench: gathered {N}-GPU image differs from the 1-GPU frame: {gather_check}", file=sys.stderr)
+        dist.barrier()
+
+    # one-shot render: no cost order from a previous identical render
+    # (the reference's use case renders once, main.cpp:292-360)
+    one_shot_ms = None
+    if args.ordering == "cost":
+        r.set_ordering("none")
+        e0, e1 = timed_render()
+        torch.cuda.synchronize(dev)
+        one_shot_ms = round(e0.elapsed_time(e1), 3)
+        r.set_ordering(args.ordering)
+
+    # The brute-force kernel's own VALU roofline: one more launch of the same
+    # rows, untimed.
     bf = None
-    if args.accel != "none":
+    if args.accel != "none" and rank == 0:
         r.set_accel("none")
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        r.render_rows(cam, W, H, SPP, DEPTH, SEED, row0, row_step, nrows, strip.data_ptr(), stream.cuda_stream)
-        e1.record(stream)
+        e0, e1 = timed_render()
         torch.cuda.synchronize(dev)
         bf_ms = e0.elapsed_time(e1)
         bf_segs = r.last_segments()
         r.set_accel(args.accel)
         bf_ach = bf_segs * FLOP_PER_SPHERE_TEST * len(world) / (bf_ms * 1e-3) / 1e12
-        bf = {"kernel_ms": round(bf_ms, 3), "achieved": round(bf_ach, 3), "frac": round(bf_ach / PEAK_FP32_TFLOPS, 4),
-              "note": "brute-force kernel (RT_ACCEL_NONE) on the same rows: the FP32 VALU roofline proper"}
+        bf = {"kernel_ms": round(bf_ms, 3), "achieved": round(bf_ach, 3), "frac": round(bf_ach / PEAK_FP32_TFLOPS, 4)}
 
-    if rank == 0 and N > 1:  # the gathered image is whole: every row rendered, none twice
-        img = rdist.unpermute([g.cpu().numpy() for g in gathered], H)
-        assert np.isfinite(img).all() and (img.reshape(H, -1).max(axis=1) > 0).all(), "incomplete gathered image"
     if rank == 0:
         samples = W * H * SPP if not args.strip_of else nrows * W * SPP
         value = samples * args.steps / elapsed / 1e6
-        flop_rank = segs * FLOP_PER_SPHERE_TEST * len(world)  # this rank's launch
-        achieved = flop_rank / (kernel_ms * 1e-3) / 1e12
+        flop_eq = segs * FLOP_PER_SPHERE_TEST * len(world)  # brute-force-equivalent work of this rank's launch
+        counts, why = None, None
+        if args.accel == "none":
+            flop_exec = flop_eq  # brute force executes every miss test
+        elif args.no_exec_counts:
+            flop_exec, why = None, "skipped (--no-exec-counts)"
+        else:
+            counts, why = executed_counts(W, H, SPP, row0, row_step, nrows, args.accel)
+            flop_exec = executed_flop(counts) if counts else None
+            if counts and counts["segments"] != segs:
+                why = f"stats build segments {counts['segments']} != product {segs}"
+                flop_exec = None
+        achieved = flop_exec / (kernel_ms * 1e-3) / 1e12 if flop_exec else None
+        eq_ach = flop_eq / (kernel_ms * 1e-3) / 1e12
         traffic = None
         pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc) and args.workload == "config2" and not args.strip_of:  # measured on config 2
+        if os.path.exists(pmc) and args.workload == "config2" and not args.strip_of and N == 1:  # measured on config 2
             try:
                 traffic = (json.load(open(pmc)).get(args.accel) or {}).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        roof = {
+            "bound": "valu",
+            "achieved": round(achieved, 3) if achieved else None,
+            "peak": PEAK_FP32_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_FP32_TFLOPS, 4) if achieved else None,
+            "traffic": traffic,
+            "work": ("executed: node slab tests x 25 + sphere miss tests x 18 FLOP, counted per lane by the "
+                     "RTMI_STATS build on the same rows" if args.accel != "none" else
+                     "executed: segments x spheres x 18 FLOP (brute force)"),
+            "flop_per_launch": flop_exec,
+            "kernel_ms": round(kernel_ms, 3),
+            "kernel_ms_max_rank": round(kernel_ms_max, 3),
+            "segments_per_launch": segs,
+            "segments_per_sample": round(total_segs / samples, 4),
+            "work_equivalent_achieved": round(eq_ach, 3),
+            "work_equivalent_frac": round(eq_ach / PEAK_FP32_TFLOPS, 4),
+            "brute_force_frac": bf["frac"] if bf else (round(eq_ach / PEAK_FP32_TFLOPS, 4) if args.accel == "none" else None),
+            "brute_force": bf,
+        }
+        if counts:
+            ls = counts["segments"]
+            ws_ = ls / 64.0
+            roof["counts"] = {
+                "node_visits_per_segment": round(counts["node_visits"] / ls, 3),
+                "leaf_sphere_tests_per_segment": round(counts["leaf_sphere_tests"] / ls, 3),
+                "big_spheres": counts["big_spheres"],
+                "node_iterations_per_wave_segment": round(counts["node_iterations_wave"] / ws_, 3),
+                "leaf_sphere_iterations_per_wave_segment": round(counts["leaf_sphere_iterations_wave"] / ws_, 3),
+                "walk_lane_utilisation": round(counts["node_visits"] / max(1, 64 * counts["node_iterations_wave"]), 4),
+                "leaf_lane_utilisation": round(counts["leaf_sphere_tests"] / max(1, 64 * counts["leaf_sphere_iterations_wave"]), 4),
+            }
+        if why:
+            roof["note"] = why
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -267,28 +545,19 @@ def main():
                 "accel": args.accel,
                 "ordering": args.ordering,
             },
-            "roofline": {
-                "bound": "valu",
-                "achieved": round(achieved, 3),
-                "peak": PEAK_FP32_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                "traffic": traffic,
-                "flop_per_launch": flop_rank,
-                "segments_per_launch": segs,
-                "segments_per_sample": round(total_segs / samples, 4),
-                "kernel_ms": round(kernel_ms, 3),
-                "kernel_ms_max_rank": round(kernel_ms_max, 3),
-                # with the BVH the FLOP count stays the brute-force figure
-                # ("work-equivalent"), so frac can pass 1
-                "work_equivalent": args.accel != "none",
-                "brute_force": bf,
-            },
+            "roofline": roof,
+            "one_shot_ms": one_shot_ms,
             "vs_baseline_ref": "published CPU rt_in_one_weekend 0.1189 Msamples/s (README.md:16-19)",
         }
+        if gather_check is not None:
+            line["gather_check"] = gather_check
         if N == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)
+        if gather_check is not None and not gather_check["bit_exact_vs_1gpu_frame"]:
+            r.close()
+            dist.destroy_process_group()
+            sys.exit(3)
     r.close()
     if N > 1:
         dist.destroy_process_group()

@@ -9,7 +9,7 @@ import os
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(REPO, "oracle", "build", "liboracle.so")
+LIB_PATH = os.environ.get("ORACLE_LIBRARY") or os.path.join(REPO, "oracle", "build", "liboracle.so")
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
 _dp = C.POINTER(C.c_double)

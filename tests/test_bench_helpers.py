@@ -45,3 +45,46 @@ def test_auto_tile_w_rule():
     assert rt.auto_tile_w(3840, 270) == 8  # 1/8 of 2160 rows: 270 = 4 * 67 + 2, no shape fills it
     assert rt.auto_tile_w(1204, 8) == 8  # columns: 8 wastes 4 per row of tiles, 16 wastes 12
     assert rt.auto_tile_w(29, 19) in (8, 16)
+
+
+def test_launch_command_starts_n_ranks_of_this_script():
+    cmd = bench.launch_command(8, ["--gpus", "8", "--steps", "3"], 29555)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd and "--master-port=29555" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"] and cmd[-5].endswith("bench.py")
+
+
+def test_gpus_beyond_visible_fails_loudly():
+    """`bench.py --gpus 2` on a box with fewer GPUs must refuse (exit 2),
+    never report a 1-GPU run as 2 (this container has no GPU)."""
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "RTMI_DIST_BACKEND")}
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 2, (p.returncode, p.stderr[-500:])
+    assert "2 GPUs asked" in p.stderr and p.stdout.strip() == ""
+
+
+def test_world_size_mismatch_fails_loudly():
+    import subprocess
+
+    env = dict(os.environ, WORLD_SIZE="4", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode != 0 and "launcher started 4 ranks" in p.stderr
+
+
+def test_socket_cpus_prefers_socket0_one_per_core():
+    # 2 sockets x 4 cores x 2 threads: cpu c -> core c % 8, socket (c % 8) // 4
+    topo = {c: ((c % 8) // 4, c % 8) for c in range(16)}
+    assert bench.socket_cpus(topo, set(range(16))) == [0, 1, 2, 3, 8, 9, 10, 11]
+    # only socket-1 CPUs allowed: that socket
+    assert bench.socket_cpus(topo, {4, 5, 12}) == [4, 5, 12]
+    assert bench.socket_cpus({}, {3, 1}) == [1, 3]
+
+
+def test_executed_flop_counts_nodes_leaves_and_big_spheres():
+    c = {"segments": 10, "node_visits": 100, "leaf_sphere_tests": 30, "big_spheres": 4}
+    assert bench.executed_flop(c) == 100 * 25 + (30 + 40) * 18

@@ -821,6 +821,14 @@ struct rt_ctx {
   int32_t chunk = 0;       // phase-1 samples per item (0 = automatic)
   int32_t tail_spp = -1;   // samples in the short-item phase (-1 = automatic)
   int32_t tail_chunk = 0;  // phase-2 samples per item (0 = automatic)
+  // cost probe: a render with no cost map of its own tile
+  // layout first renders probe_spp samples per pixel into its output strip,
+  // counting world.hit per tile, and orders its tiles by those counts.
+  // RTMI_ORDER_PROBE: 0 = never probe (order by the previous identical render
+  // only), 1 = probe when no map of this layout exists (default), 2 = probe
+  // before every render (no state carried between renders)
+  int32_t probe_mode = std::getenv("RTMI_ORDER_PROBE") ? std::atoi(std::getenv("RTMI_ORDER_PROBE")) : 1;
+  bool probing = false;
 };
 
 namespace rtmi {
@@ -1394,6 +1402,19 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
         HIP_TRY(hipMalloc(&ctx->sort_tmp, need));
         ctx->sort_tmp_bytes = need;
       }
+    }
+    const bool have_map = ctx->cost_valid && std::equal(key, key + 6, ctx->cost_key);
+    // Probe: 1 sample per pixel (2 from 256 spp up) rendered into the output
+    // strip (overwritten by this render) counts world.hit per tile, about
+    // 1/250 of the render's work; the render then dispatches by those counts.
+    if (!ctx->probing && strip && !pass_accum && spp >= 16 &&
+        (ctx->probe_mode == 2 || (ctx->probe_mode == 1 && !have_map))) {
+      ctx->probing = true;
+      const int rc = render_rows_impl(ctx, cam, W, H, spp >= 256 ? 2 : 1, max_depth, seed, row0, row_step, nrows, strip,
+                                      st, s_base, nullptr);
+      ctx->probing = false;
+      if (rc) return rc;
+      HIP_TRY(hipMemsetAsync(ctx->segments, 0, 8 * sizeof(unsigned long long), st));  // count this render only
     }
     if (ctx->cost_valid && std::equal(key, key + 6, ctx->cost_key)) {
       size_t bytes = ctx->sort_tmp_bytes;

@@ -149,10 +149,12 @@ int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind);
 enum { RT_ACCEL_NONE = 0, RT_ACCEL_BVH = 1 };
 
 /* Dispatch order.  RT_ORDER_COST (default): every render counts world.hit
- * calls per tile, and the next render with the same tile layout dispatches
- * its tiles most-expensive-first (a GPU radix sort of those counts), so the
- * end of the launch is cheap work.  RT_ORDER_NONE: tiles in image order.
- * Never changes the image. */
+ * calls per tile and dispatches its tiles most-expensive-first (a GPU radix
+ * sort of per-tile counts), so the end of the launch is cheap work.  The
+ * counts come from the previous render with the same tile layout, or — when
+ * there is none (a one-shot render) — from a probe pass of 1-2 samples per
+ * pixel run first on the same stream (~1/250 of the work).  RT_ORDER_NONE:
+ * tiles in image order.  Never changes the image. */
 enum { RT_ORDER_NONE = 0, RT_ORDER_COST = 1 };
 int rt_ctx_set_ordering(rt_ctx *ctx, int32_t ordering);
 int rt_ctx_set_accel(rt_ctx *ctx, int32_t accel);

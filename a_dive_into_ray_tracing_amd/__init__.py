@@ -226,6 +226,13 @@ class Renderer:
         check(self.L.rt_ctx_last_segments(self._h, C.byref(v)), "rt_ctx_last_segments")
         return v.value
 
+    def last_schedule(self):
+        """Diagnostic: the last launch's schedule as a dict (rt_ctx_last_schedule)."""
+        v = (C.c_int32 * 8)()
+        check(self.L.rt_ctx_last_schedule(self._h, v), "rt_ctx_last_schedule")
+        keys = ("tile_w", "chunk", "items_per_tile", "tail_items_per_tile", "block_flush", "block_pool", "persistent", "bvh")
+        return dict(zip(keys, list(v)))
+
     def synchronize(self):
         check(self.L.rt_ctx_synchronize(self._h), "rt_ctx_synchronize")
 

@@ -137,7 +137,15 @@ __device__ unsigned g_trace_n;
 #endif
 constexpr int kPairGroup = RTMI_PAIR_GROUP;  // sphere pairs per scalar-load group
 
-__device__ __forceinline__ int64_t to_fixed(float c) { return int64_t(c * 4294967296.0f); }
+// Per-sample colour -> int64 fixed point (2^-32).  Guarded: NaN -> 0 and
+// the value clamped to [-64, 64], so the conversion is always defined and a
+// sum of up to 2^24 samples cannot overflow (64 * 2^24 * 2^32 = 2^62);
+// every scene here stays far inside (RTIOW colours are <= 1).  The oracle
+// applies the identical guard.
+__device__ __forceinline__ int64_t to_fixed(float c) {
+  const float g = c == c ? (c > 64.0f ? 64.0f : (c < -64.0f ? -64.0f : c)) : 0.0f;
+  return int64_t(g * 4294967296.0f);
+}
 __device__ __forceinline__ float from_fixed(int64_t v) { return float(v) * 0x1p-32f; }
 
 // Grid-kernel block shape.  A block holds its wave slots (and LDS) until its
@@ -178,12 +186,12 @@ __global__ __launch_bounds__(64 * GridShape<BVH>::waves, GridShape<BVH>::per_eu)
   if (item < a.tiles * a.nch1) {
     tile = item / a.nch1;
     s0 = (item - tile * a.nch1) * a.chunk1;
-    ns = min(a.chunk1, a.spp1 - s0);
+    ns = max(0, min(a.chunk1, a.spp1 - s0));  // 0: an empty item of the automatic schedule
   } else {
     const int i2 = item - a.tiles * a.nch1;
     tile = i2 / a.nch2;
     s0 = a.spp1 + (i2 - tile * a.nch2) * a.chunk2;
-    ns = min(a.chunk2, a.spp - s0);
+    ns = max(0, min(a.chunk2, a.spp - s0));
   }
   if (a.tile_order) tile = a.tile_order[tile];  // expensive tiles first
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
@@ -394,12 +402,12 @@ __device__ __forceinline__ ItemDesc describe_item(const RenderArgs &a, int item)
   if (item < a.tiles * a.nch1) {
     tile = item / a.nch1;
     s0 = (item - tile * a.nch1) * a.chunk1;
-    ns = min(a.chunk1, a.spp1 - s0);
+    ns = max(0, min(a.chunk1, a.spp1 - s0));
   } else {
     const int i2 = item - a.tiles * a.nch1;
     tile = i2 / a.nch2;
     s0 = a.spp1 + (i2 - tile * a.nch2) * a.chunk2;
-    ns = min(a.chunk2, a.spp - s0);
+    ns = max(0, min(a.chunk2, a.spp - s0));
   }
   if (a.tile_order) tile = a.tile_order[tile];  // expensive tiles first
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
@@ -806,8 +814,11 @@ struct rt_ctx {
   // block-level accumulator flush of the automatic grid schedule (same image;
   // RTMI_BLOCK_FLUSH=0 in the environment turns it off, for A/B and tests)
   bool block_flush = !(std::getenv("RTMI_BLOCK_FLUSH") && std::getenv("RTMI_BLOCK_FLUSH")[0] == '0');
-  // block-shared job pool of block_flush launches (same image; RTMI_BLOCK_POOL=0 turns it off)
-  bool block_pool = !(std::getenv("RTMI_BLOCK_POOL") && std::getenv("RTMI_BLOCK_POOL")[0] == '0');
+  // block-shared job pool of block_flush launches (same image; measured
+  // neutral, DESIGN.md §5, so off unless RTMI_BLOCK_POOL=1)
+  bool block_pool = std::getenv("RTMI_BLOCK_POOL") && std::getenv("RTMI_BLOCK_POOL")[0] == '1';
+  // the schedule of the last launch (rt_ctx_last_schedule, for tests)
+  int32_t last_sched[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned *cost_prev = nullptr, *cost_cur = nullptr, *cost_sorted = nullptr;
   int32_t *order = nullptr, *iota = nullptr;
   size_t cost_cap = 0;  // tiles
@@ -1323,14 +1334,18 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   tail = std::min(tail, spp);
   const int32_t spp1 = spp - tail;
   const int64_t grid_wpb = bvh ? GridShape<true>::waves : GridShape<false>::waves;
+  int32_t nch1 = spp1 > 0 ? (spp1 + chunk1 - 1) / chunk1 : 0;
   if (ctx->chunk <= 0 && !persistent && tail == 0 && spp1 >= grid_wpb) {
-    // automatic grid schedule: a multiple of the block's waves per tile, so a
-    // block's items share a tile and it flushes once (block_flush)
+    // automatic grid schedule: exactly a multiple of the block's waves items
+    // per tile, so a block's items share a tile and it flushes once
+    // (block_flush).  chunk1 = ceil(spp1 / n1) can leave the last items of a
+    // tile empty (spp1 = 5 on 4 waves: 2, 2, 1, 0 samples); an empty item's
+    // wave takes no job and only joins the block's flush.
     int64_t n1 = (spp1 + chunk1 - 1) / chunk1;
     n1 = (n1 + grid_wpb - 1) / grid_wpb * grid_wpb;
     chunk1 = int32_t((spp1 + n1 - 1) / n1);
+    nch1 = int32_t(n1);
   }
-  const int32_t nch1 = spp1 > 0 ? (spp1 + chunk1 - 1) / chunk1 : 0;
   chunk2 = std::min(chunk2, std::max(tail, 1));
   const int32_t nch2 = tail > 0 ? (tail + chunk2 - 1) / chunk2 : 0;
   const int64_t items = tiles * (int64_t(nch1) + nch2);
@@ -1345,6 +1360,10 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   a.tiles = int32_t(tiles); a.spp1 = spp1; a.chunk1 = chunk1; a.nch1 = nch1; a.chunk2 = chunk2; a.nch2 = nch2;
   a.block_flush = !persistent && nch2 == 0 && nch1 % grid_wpb == 0 && ctx->block_flush;
   a.block_pool = a.block_flush && ctx->block_pool;
+  if (!ctx->probing) {
+    const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush, a.block_pool, persistent ? 1 : 0, bvh ? 1 : 0};
+    std::copy(sched, sched + 8, ctx->last_sched);
+  }
   a.s_base = s_base;
   a.out_elems = uint64_t(nvalid) * uint64_t(W) * 3;
   const bool chunked = pass_accum || nch1 + nch2 > 1;
@@ -1719,6 +1738,12 @@ RTMI_EXPORT int rt_replay_worker(rt_ctx *ctx, const rt_camera *cam, int32_t W, i
   if (e != hipSuccess) return set_error(RT_EHIP, "rt_replay_worker: %s", hipGetErrorString(e));
   for (int k = 0; k < n_jobs; k++)
     if (draws_used[k] < 0) return set_error(RT_ESTREAM, "job %d ran out of stream values", k);
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_ctx_last_schedule(rt_ctx *ctx, int32_t *out8) {
+  if (!ctx || !out8) return set_error(RT_EINVAL, "null");
+  std::copy(ctx->last_sched, ctx->last_sched + 8, out8);
   return RT_OK;
 }
 

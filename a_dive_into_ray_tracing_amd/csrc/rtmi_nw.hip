@@ -62,7 +62,11 @@ constexpr size_t kLdsBudget = size_t(RTMI_NW_LDS_KB) * 1024;  // grid kernel: st
 constexpr int kPWaves = 16;                                   // persistent kernel: waves per block (one per CU)
 constexpr size_t kPLdsBudget = 136 * 1024;                    // persistent kernel: staged bytes (+ 24 KB accumulators)
 
-__device__ __forceinline__ int64_t fixed(float c) { return int64_t(c * 4294967296.0f); }
+// NaN -> 0, clamped to [-64, 64]: as rtmi_device.hip to_fixed (and the oracle)
+__device__ __forceinline__ int64_t fixed(float c) {
+  const float g = c == c ? (c > 64.0f ? 64.0f : (c < -64.0f ? -64.0f : c)) : 0.0f;
+  return int64_t(g * 4294967296.0f);
+}
 
 template <bool LDS_NODES, bool LDS_OBJS>
 __device__ __forceinline__ void stage_scene(const View &sc) {
@@ -316,6 +320,13 @@ struct rt_nw_ctx {
   unsigned long long *segments = nullptr;
   unsigned *counter = nullptr;  // persistent kernel's work-item counter
   int32_t persist_blocks = 0;   // resident 16-wave blocks (CUs x blocks per CU)
+  // samples per work item forced by RTMI_NW_CHUNK (A/B only; 0 = automatic),
+  // read when the context is created
+  int32_t env_chunk = std::getenv("RTMI_NW_CHUNK") ? std::atoi(std::getenv("RTMI_NW_CHUNK")) : 0;
+  // the buffers above are shared by every render of the context: a render on
+  // another stream first waits for the end of the last one (as rt_ctx)
+  hipStream_t last_stream = nullptr;
+  hipEvent_t last_done = nullptr;
 };
 
 namespace {
@@ -389,6 +400,7 @@ RTMI_EXPORT int rt_nw_ctx_create(int32_t device, rt_nw_ctx **out) {
   auto ctx = std::make_unique<rt_nw_ctx>();
   ctx->device = device;
   HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&ctx->last_done, hipEventDisableTiming));
   if (int rc = alloc_copy<unsigned long long>(&ctx->segments, nullptr, 1)) return rc;
   HIP_TRY(hipMemset(ctx->segments, 0, sizeof(unsigned long long)));
   if (int rc = alloc_copy<unsigned>(&ctx->counter, nullptr, 1)) return rc;
@@ -411,6 +423,7 @@ RTMI_EXPORT int rt_nw_ctx_destroy(rt_nw_ctx *ctx) {
                   (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments, (void *)ctx->counter})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(ctx->stream);
+  if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
   delete ctx;
   return RT_OK;
 }
@@ -524,29 +537,37 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
   a.nrows_valid = valid;
   a.tiles_x = (W + 7) / 8;
   a.tiles = a.tiles_x * ((valid + 7) / 8);
+  // kernel shape: persistent when the nodes fit one CU's LDS budget, else grid
+  const size_t node_bytes = size_t(ctx->nnodes) * 32, obj_bytes = size_t(ctx->nobj) * (sizeof(DevObj) + 4);
+  const bool persist = RTMI_NW_PERSIST && ctx->nnodes > 0 && node_bytes <= kPLdsBudget && ctx->persist_blocks > 0;
   // samples per work item (same image for any size; RTMI_NW_CHUNK overrides,
-  // for A/B).  Automatic: ~80 items per resident wave of the persistent
-  // kernel, 4..32 samples: the final scene (fog, lights: long and uneven paths)
-  // at 256 spp runs 329 ms with 8, 433 with 32; at 1024 spp 1215 ms with 24,
-  // 1205 with 32, 1308 with 8 — the item count, not the size, sets its tail
-  // (profiles/r01/session6/nw_chunk.txt)
-  static const int env_chunk = std::getenv("RTMI_NW_CHUNK") ? std::atoi(std::getenv("RTMI_NW_CHUNK")) : 0;
+  // for A/B).  Persistent kernel: ~80 items per resident wave, 4..32 samples:
+  // the final scene (fog, lights: long and uneven paths) at 256 spp runs 329
+  // ms with 8, 433 with 32; at 1024 spp 1215 ms with 24, 1205 with 32, 1308
+  // with 8 — the item count, not the size, sets its tail
+  // (profiles/r01/session6/nw_chunk.txt).  Grid kernel: 32.
   int64_t chunk = 32;
-  if (ctx->persist_blocks > 0) {
+  if (persist) {
     const int64_t waves = int64_t(ctx->persist_blocks) * kPWaves;
     chunk = std::min<int64_t>(32, std::max<int64_t>(4, int64_t(a.tiles) * spp / (80 * waves)));
   }
-  a.chunk = std::min<int64_t>(spp, env_chunk > 0 ? env_chunk : chunk);
+  a.chunk = std::min<int64_t>(spp, ctx->env_chunk > 0 ? ctx->env_chunk : chunk);
   a.nch = (spp + a.chunk - 1) / a.chunk;
   if (int64_t(a.tiles) * a.nch >= (int64_t(1) << 31) - kWaves) return set_error(RT_EINVAL, "render too large");
   a.n_items = a.tiles * a.nch;
+  // the context's buffers (accumulator, counters) are shared by every render:
+  // a render on another stream first waits for the last one
+  if (ctx->last_stream && ctx->last_stream != st) HIP_TRY(hipStreamWaitEvent(st, ctx->last_done, 0));
+  ctx->last_stream = st;
+  struct MarkDone {  // record the end of this render's work, whatever path returns
+    rt_nw_ctx *c;
+    hipStream_t s;
+    ~MarkDone() { (void)hipEventRecord(c->last_done, s); }
+  } mark_done{ctx, st};
   if (valid < nrows)  // rows past H: zero
     HIP_TRY(hipMemsetAsync(dev_strip + size_t(valid) * W * 3, 0, size_t(nrows - valid) * W * 3 * sizeof(float), st));
   HIP_TRY(hipMemsetAsync(ctx->segments, 0, sizeof(unsigned long long), st));
   const View v = view_of(ctx);
-  const size_t node_bytes = size_t(ctx->nnodes) * 32, obj_bytes = size_t(ctx->nobj) * (sizeof(DevObj) + 4);
-  // persistent: everything that fits one CU's LDS budget; else the grid kernel
-  const bool persist = RTMI_NW_PERSIST && ctx->nnodes > 0 && node_bytes <= kPLdsBudget && ctx->persist_blocks > 0;
   const bool p_objs = RTMI_NW_LDS_OBJS && persist && node_bytes + obj_bytes <= kPLdsBudget;
   const bool lds_nodes = !persist && ctx->nnodes > 0 && node_bytes <= kLdsBudget,
              lds_objs = RTMI_NW_LDS_OBJS && lds_nodes && node_bytes + obj_bytes <= kLdsBudget;

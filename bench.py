@@ -331,6 +331,9 @@ def main():
     ap.add_argument("--ordering", choices=["cost", "none"], default="cost")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-exec-counts", action="store_true", help="skip the RTMI_STATS work count (roofline.frac null)")
+    ap.add_argument("--timed-only", action="store_true",
+                    help="no untimed side launches (one-shot, brute force, gather check): for profiler runs whose "
+                         "kernel averages must cover only the warmup + timed launches")
     ap.add_argument("--workload", choices=list(RTIOW_WORKLOADS) + ["nw_motion_blur", "nw_final"], default="config2")
     ap.add_argument("--nw-spp", type=int, default=0, help="spp of the nw_* workloads (default: 500 / 1024)")
     ap.add_argument("--strip-of", type=int, default=0,
@@ -428,7 +431,7 @@ def main():
     # whole frame, bit for bit (every pixel's stream is keyed by its
     # coordinates, so the partition must not change a single value)
     gather_check = None
-    if N > 1:
+    if N > 1 and not args.timed_only:
         if rank == 0:
             full = torch.empty((H, W, 3), dtype=torch.float32, device=dev)
             e0, e1 = timed_render((0, 1, H), full)
@@ -446,7 +449,7 @@ def main():
     # no cost map from a previous identical render, so the library runs its
     # probe pass first (included); and the same render in plain image order
     one_shot = None
-    if args.ordering == "cost":
+    if args.ordering == "cost" and not args.timed_only:
         r.set_ordering("cost")  # forgets the previous render's cost map
         e0, e1 = timed_render()
         r.set_ordering("none")
@@ -458,7 +461,7 @@ def main():
     # The brute-force kernel's own VALU roofline: one more launch of the same
     # rows, untimed.
     bf = None
-    if args.accel != "none" and rank == 0:
+    if args.accel != "none" and rank == 0 and not args.timed_only:
         r.set_accel("none")
         e0, e1 = timed_render()
         torch.cuda.synchronize(dev)

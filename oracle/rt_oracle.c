@@ -391,7 +391,12 @@ int32_t or_ref_scatter(int32_t kind, const double mat[4], const double din[3], c
 /* fast-mode API                                                            */
 /* ---------------------------------------------------------------------- */
 /* per-sample colour -> int64 fixed point, 2^-32 units (truncation) */
-static inline int64_t to_fixed(float c) { return (int64_t)(c * 4294967296.0f); }
+/* the kernel's guarded conversion (rtmi_device.hip to_fixed): NaN -> 0,
+ * clamped to [-64, 64] so the cast is defined and 2^24-sample sums fit */
+static inline int64_t to_fixed(float c) {
+  const float g = c == c ? (c > 64.0f ? 64.0f : (c < -64.0f ? -64.0f : c)) : 0.0f;
+  return (int64_t)(g * 4294967296.0f);
+}
 static inline float from_fixed(int64_t v) { return (float)v * 0x1p-32f; }
 
 static int32_t fast_rows(const or_scene *s, const or_camera *c, int32_t W, int32_t H, int32_t spp,

@@ -25,6 +25,27 @@ def _ensure_built():
 _ensure_built()
 
 
+def record_parity_stats(name, values):
+    """Statistical-tier numbers of a GPU test -> gpurun_out/parity_stats.json
+    (merged back from the GPU box; copied to profiles/ per round), so the
+    bias / MAE / RMSE / tile-max and convergence ratios are on record, not
+    only pass/fail."""
+    import json
+
+    out = os.path.join(REPO, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    path = os.path.join(out, "parity_stats.json")
+    data = {}
+    if os.path.exists(path):
+        try:
+            data = json.load(open(path))
+        except Exception:
+            data = {}
+    data[name] = {k: (round(float(v), 6) if isinstance(v, (float, int)) else v) for k, v in values.items()}
+    with open(path, "w") as f:
+        json.dump(data, f, indent=1, sort_keys=True)
+
+
 @pytest.fixture(scope="session")
 def golden_dir():
     return os.path.join(REPO, "tests", "golden")

@@ -113,3 +113,22 @@ def test_direct_point_in_disk():
     assert r.max() < 1.0 and not p[:, 2].any()
     for q in (0.25, 0.5, 0.75, 0.9):
         assert abs((r < q).mean() - q ** 2) < 0.004
+
+
+def test_fixed_point_guard_non_finite_colours():
+    """The oracle's fixed-point conversion (mirrored by the kernels' to_fixed):
+    NaN -> 0, values clamped to [-64, 64], so sums stay finite.  A NaN albedo
+    and an overflowing one (1e30: attenuation -> inf) produce such colours."""
+    import ctypes as C
+
+    import a_dive_into_ray_tracing_amd as rt
+
+    world = rt.learn_scene()
+    world.mat_params[1, :3] = [np.nan, 0.5, 0.5]
+    world.mat_params[4, :3] = [1e30, 1e30, 1e30]
+    cam = rt.learn_camera(40 / 24)
+    c = O.OrCamera()
+    C.memmove(C.byref(c), C.byref(cam), C.sizeof(c))
+    out = O.fast_render(O.Scene(world.center_radius, world.mat_kind, world.mat_params), c, 40, 24, 8, 50, 1984)
+    assert np.isfinite(out).all()
+    assert out.max() == 64.0 * 8  # a pixel whose 8 samples all saturate

@@ -163,4 +163,10 @@ def test_config4_convergence(renderer):
     e5000 = np.sqrt(((rt.quantize(imgs[5000], 5000) - ref) ** 2).mean())
     print(f"RMSE vs gallery (500 spp reference): ours@500 {e500:.3f}, ours@5000 {e5000:.3f}")
     # the reference's own noise at 500 spp is RMSE 1.795 / sqrt(2) = 1.27 levels
+    from conftest import record_parity_stats
+
+    record_parity_stats("config4_convergence", {
+        "rms_seed_to_seed_50": rms[50], "rms_seed_to_seed_500": rms[500], "rms_seed_to_seed_5000": rms[5000],
+        "ratio_50_500": r1, "ratio_500_5000": r2, "ideal_ratio": np.sqrt(10), "rmse_vs_gallery_at_500": e500,
+        "rmse_vs_gallery_at_5000": e5000, "thresholds": "ratios within 12% of sqrt(10); RMSE@5000 < RMSE@500 and < 1.5"})
     assert e5000 < e500 and e5000 < 1.5

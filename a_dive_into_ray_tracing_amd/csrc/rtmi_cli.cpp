@@ -74,6 +74,10 @@ int main(int argc, char **argv) {
   if (learn && spp == 500) spp = 100;                             // main.cpp:189
 
   if (!checkpoint.empty() && pass_spp <= 0) { std::fprintf(stderr, "--checkpoint needs --pass-spp\n"); return 2; }
+  if (W < 2 || H < 2 || int64_t(W) * H > (int64_t(1) << 31) || spp < 1 || depth < 0 || gpus < 0 || pass_spp < 0) {
+    std::fprintf(stderr, "rtmi_render: bad size (W, H >= 2, W*H <= 2^31, spp >= 1, depth >= 0, gpus >= 0)\n");
+    return 2;
+  }
   int32_t n = 0;
   int rc = 0;
   if (!scene_file.empty() && (rc = rt_scene_read(scene_file.c_str(), nullptr, nullptr, nullptr, 0, &n)) && n == 0)

@@ -59,6 +59,17 @@ RTMI_EXPORT int rt_camera_init(rt_camera *cam, const double lookfrom[3], const d
                               const double vup[3], double vfov_deg, double aspect_ratio,
                               double aperture, double focus_dist) {
   if (!cam || !lookfrom || !lookat || !vup) return set_error(RT_EINVAL, "rt_camera_init: null argument");
+  {  // a camera the reference would build from NaNs is refused instead
+    bool finite = std::isfinite(vfov_deg) && std::isfinite(aspect_ratio) && std::isfinite(aperture) &&
+                  std::isfinite(focus_dist);
+    for (int a = 0; a < 3; ++a) finite = finite && std::isfinite(lookfrom[a]) && std::isfinite(lookat[a]) && std::isfinite(vup[a]);
+    const D3 dv = d3(lookfrom[0] - lookat[0], lookfrom[1] - lookat[1], lookfrom[2] - lookat[2]);
+    const D3 side = cross(d3(vup[0], vup[1], vup[2]), dv);
+    if (!finite || !(vfov_deg > 0 && vfov_deg < 180) || !(aspect_ratio > 0) || aperture < 0 || len(dv) == 0 ||
+        len(side) == 0)
+      return set_error(RT_EINVAL, "rt_camera_init: degenerate camera (lookfrom == lookat, vup parallel to the "
+                                  "view direction, vfov outside (0, 180), aspect <= 0 or a non-finite value)");
+  }
   const double pi = 3.1415926535897932385;            // rtweekend.h:16
   double theta = vfov_deg * pi / 180.0;               // degree_to_radians rtweekend.h:19
   double h = std::tan(theta / 2);
@@ -182,7 +193,9 @@ RTMI_EXPORT int rt_scene_learn(double *center_radius, int32_t *mat_kind, double 
 // ---------------------------------------------------------------------------
 static inline int quant(float sum, double scale) {
   double c = std::sqrt(scale * static_cast<double>(sum));
-  if (c < 0.0) c = 0.0;      // clamp rtweekend.h:31-37 (NaN passes through, as there)
+  // clamp rtweekend.h:31-37.  A NaN passes the reference's clamp and its
+  // int cast is undefined there; here it is 0 (negative sums give NaN too)
+  if (!(c >= 0.0)) c = 0.0;
   if (c > 0.999) c = 0.999;
   return static_cast<int>(256 * c);
 }
@@ -288,6 +301,10 @@ RTMI_EXPORT int rt_scene_read(const char *path, double *center_radius, int32_t *
                                 &v[6], &v[7], &v[8]);
     if (got <= 0) continue;  // blank / comment
     if (got == 1 && declared < 0 && w.n == 0 && !w.overflow) {
+      if (!(v[0] >= 0 && v[0] <= 2147483647.0 && v[0] == std::floor(v[0]))) {  // range-checked before the cast
+        rc = set_error(RT_EINVAL, "%s:%d: bad sphere count", path, lineno);
+        break;
+      }
       declared = long(v[0]);
       continue;
     }
@@ -306,6 +323,7 @@ RTMI_EXPORT int rt_scene_read(const char *path, double *center_radius, int32_t *
   if (rc) return rc;
   if (declared >= 0 && declared != w.n)
     return set_error(RT_EINVAL, "%s: header says %ld spheres, file has %d", path, declared, w.n);
+  if (w.n == 0) return set_error(RT_EINVAL, "%s: no spheres", path);
   *n_out = w.n;
   if (w.overflow) return set_error(RT_EINVAL, "rt_scene_read: cap %d too small for %d spheres", cap, w.n);
   return RT_OK;

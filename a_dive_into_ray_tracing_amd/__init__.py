@@ -196,7 +196,7 @@ class Renderer:
     def set_ordering(self, ordering="cost"):
         check(self.L.rt_ctx_set_ordering(self._h, self.ORDERINGS[ordering]), "rt_ctx_set_ordering")
 
-    ACCELS = {"none": 0, "bvh": 1}  # RT_ACCEL_* (include/rtmi.h)
+    ACCELS = {"none": 0, "bvh": 1, "grid": 2}  # RT_ACCEL_* (include/rtmi.h)
 
     def set_accel(self, accel="none"):
         check(self.L.rt_ctx_set_accel(self._h, self.ACCELS[accel]), "rt_ctx_set_accel")
@@ -206,6 +206,12 @@ class Renderer:
         nb, nn = C.c_int32(), C.c_int32()
         check(self.L.rt_ctx_accel_info(self._h, C.byref(nb), C.byref(nn)), "rt_ctx_accel_info")
         return nb.value, nn.value
+
+    def grid_info(self):
+        """((nx, ny, nz) cells, references, LDS bytes) of the scene's uniform grid."""
+        dims, nr, lds = (C.c_int32 * 3)(), C.c_int32(), C.c_int32()
+        check(self.L.rt_ctx_grid_info(self._h, dims, C.byref(nr), C.byref(lds)), "rt_ctx_grid_info")
+        return tuple(dims), nr.value, lds.value
 
     def render(self, cam, W, H, spp, max_depth=50, seed=1984):
         """Whole image, host float32 sums [H, W, 3], row 0 = bottom (main.cpp:274)."""

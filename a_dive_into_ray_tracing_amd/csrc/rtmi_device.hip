@@ -163,13 +163,15 @@ template <bool BVH> struct GridShape {
   static constexpr int waves = BVH ? RTMI_BVH_WAVES : kWavesPerBlock;
   static constexpr int per_eu = BVH ? 8 : RTMI_WAVES_PER_EU;
 };
-template <int TW, bool CHUNKED, bool BVH>
-__global__ __launch_bounds__(64 * GridShape<BVH>::waves, GridShape<BVH>::per_eu) void render_kernel(
+// ACC: 0 brute force, 1 BVH, 2 uniform grid (RT_ACCEL_*); the accelerated
+// kernels stage their structure in LDS and share the block shape.
+template <int TW, bool CHUNKED, int ACC>
+__global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0>::per_eu) void render_kernel(
     const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1,
     const SpherePair *__restrict__ pairs, RenderArgs a, unsigned long long *__restrict__ accum,
     float *__restrict__ out, unsigned long long *__restrict__ segments) {
   constexpr int TH = 64 / TW;
-  constexpr int WPB = GridShape<BVH>::waves;
+  constexpr int WPB = GridShape<ACC != 0>::waves;
   __shared__ unsigned long long acc[WPB][3][64];
   __shared__ unsigned long long wave_segs[WPB];
   __shared__ unsigned pool_next;  // block pool: next unclaimed job
@@ -178,7 +180,8 @@ __global__ __launch_bounds__(64 * GridShape<BVH>::waves, GridShape<BVH>::per_eu)
   const int item = blockIdx.x * WPB + wave;
   const bool pool = CHUNKED && a.block_pool;  // block-uniform (implies block_flush)
   if (pool && threadIdx.x == 0) pool_next = 64 * WPB;
-  if constexpr (BVH) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
+  if constexpr (ACC == 1) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
+  else if constexpr (ACC == 2) stage_grid(a.acc);
   else if (pool) __syncthreads();
   if (item >= a.n_items) return;  // wave-uniform; no block barrier follows
 
@@ -260,10 +263,16 @@ __global__ __launch_bounds__(64 * GridShape<BVH>::waves, GridShape<BVH>::per_eu)
       const unsigned long long cyc0 = __builtin_amdgcn_s_memtime();
 #endif
       int k;
-      if constexpr (BVH) {
+      if constexpr (ACC == 1) {
         k = hit_world_bvh<kBigGroup>(a.acc, o, d, t
 #if RTMI_STATS
                                       , bvh_stats
+#endif
+        );
+      } else if constexpr (ACC == 2) {
+        k = hit_world_grid<kBigGroup>(a.acc, o, d, t
+#if RTMI_STATS
+                                       , bvh_stats
 #endif
         );
       } else {
@@ -423,7 +432,7 @@ __device__ __forceinline__ ItemDesc describe_item(const RenderArgs &a, int item)
   return r;
 }
 
-template <int TW, bool CHUNKED, bool BVH>
+template <int TW, bool CHUNKED, int ACC>
 __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void render_persistent(
     const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1,
     const SpherePair *__restrict__ pairs, RenderArgs a, unsigned long long *__restrict__ accum,
@@ -433,7 +442,8 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
   __shared__ unsigned slot_segs[kWavesPerBlock][2];  // world.hit calls of each slot's item (tile cost)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if constexpr (BVH) stage_bvh(a.acc);
+  if constexpr (ACC == 1) stage_bvh(a.acc);
+  else if constexpr (ACC == 2) stage_grid(a.acc);
   if (lane < 2) slot_segs[wave][lane] = 0;
   for (int s = 0; s < 2; ++s)
     for (int c = 0; c < 3; ++c) acc[wave][s][c][lane] = 0;
@@ -580,10 +590,16 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
       const unsigned long long cyc0 = __builtin_amdgcn_s_memtime();
 #endif
       int k;
-      if constexpr (BVH) {
+      if constexpr (ACC == 1) {
         k = hit_world_bvh<kBigGroup>(a.acc, o, d, t
 #if RTMI_STATS
                                       , bvh_stats
+#endif
+        );
+      } else if constexpr (ACC == 2) {
+        k = hit_world_grid<kBigGroup>(a.acc, o, d, t
+#if RTMI_STATS
+                                       , bvh_stats
 #endif
         );
       } else {
@@ -674,10 +690,12 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
 
 // Closest hit of n given rays by the brute-force loop and by the BVH
 // (validation: rt_ctx_debug_hits).  rays = {o.xyz, d.xyz} per ray.
+template <int ACC>
 __global__ __launch_bounds__(256) void debug_hit_kernel(const SpherePair *__restrict__ pairs, int32_t npairs, Accel acc,
                                                        const float *__restrict__ rays, int32_t n,
                                                        int32_t *__restrict__ out_idx, float *__restrict__ out_t) {
-  stage_bvh(acc);
+  if constexpr (ACC == 1) stage_bvh(acc);
+  else stage_grid(acc);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const V3<float> o = mk(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
@@ -686,13 +704,13 @@ __global__ __launch_bounds__(256) void debug_hit_kernel(const SpherePair *__rest
 #if RTMI_STATS
   unsigned st[4] = {0, 0, 0, 0}, bst[5] = {0, 0, 0, 0, 0};
   out_idx[2 * i] = hit_world_packed<kPairGroup>(pairs, npairs, o, d, t0, st);
-  out_idx[2 * i + 1] = acc.nnodes ? hit_world_bvh<kBigGroup>(acc, o, d, t1, bst) : -2;
+  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1, bst) : hit_world_grid<kBigGroup>(acc, o, d, t1, bst);
 #else
   out_idx[2 * i] = hit_world_packed<kPairGroup>(pairs, npairs, o, d, t0);
-  out_idx[2 * i + 1] = acc.nnodes ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : -2;
+  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup>(acc, o, d, t1);
 #endif
   out_t[2 * i] = t0;
-  out_t[2 * i + 1] = acc.nnodes ? t1 : 0.f;
+  out_t[2 * i + 1] = t1;
 }
 
 __global__ void finalize_kernel(const unsigned long long *__restrict__ accum, float *__restrict__ out, size_t n) {
@@ -808,6 +826,14 @@ struct rt_ctx {
   int32_t *bvh_idx = nullptr;
   int32_t nbvh_sph = 0;
   int32_t resident_blocks_bvh = 0;  // persistent grid with the BVH's LDS
+  // uniform grid, built by rt_ctx_set_scene beside the BVH
+  float4 *grid_sph = nullptr;
+  int32_t *grid_idx = nullptr;
+  uint16_t *grid_cell_start = nullptr, *grid_refs = nullptr;
+  GridDesc grid{};
+  int32_t ngrid_sph = 0;
+  bool grid_ok = false;
+  int32_t resident_blocks_grid = 0;
   // cost-ordered dispatch: per-tile world.hit counts of the
   // last render with the same tile layout order the next one's tiles
   int32_t ordering = RT_ORDER_COST;
@@ -941,7 +967,8 @@ RTMI_EXPORT int rt_ctx_destroy(rt_ctx *ctx) {
                   (void *)ctx->sh164, (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments, (void *)ctx->pairs, (void *)ctx->counter, (void *)ctx->pass_accum,
                   (void *)ctx->big_pairs, (void *)ctx->big_idx, (void *)ctx->nodes, (void *)ctx->bvh_sph, (void *)ctx->bvh_idx,
                   (void *)ctx->cost_prev, (void *)ctx->cost_cur, (void *)ctx->cost_sorted, (void *)ctx->order,
-                  (void *)ctx->iota, ctx->sort_tmp})
+                  (void *)ctx->iota, ctx->sort_tmp, (void *)ctx->grid_sph, (void *)ctx->grid_idx,
+                  (void *)ctx->grid_cell_start, (void *)ctx->grid_refs})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(ctx->stream);
   if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
@@ -1056,6 +1083,85 @@ struct BvhBuilder {
 };
 }  // namespace
 
+namespace {
+// Uniform grid over the small spheres.  The box of their
+// margin-grown boxes (the BVH's margins) is cut into cells of about
+// RTMI_GRID_CELLS (default 1) cells per sphere, as near cubic as the box
+// allows (the final scene's thin layer of spheres: 30 x 1 x 30 cells); every
+// sphere is listed in every cell its grown box overlaps.  Cell boundaries are
+// the float values g0 + c*h the device computes, so host and device agree to
+// a rounding error far below the margins.
+struct GridBuild {
+  GridDesc desc{};
+  std::vector<float4> sph;
+  std::vector<int32_t> idx;
+  std::vector<uint16_t> cell_start, refs;
+};
+bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, GridBuild &out) {
+  const char *env = std::getenv("RTMI_GRID_CELLS");
+  const double per_sphere = env && std::atof(env) > 0 ? std::atof(env) : 1.0;
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int32_t k : small) {
+    const double *c = b.cr + 4 * k, R = std::fabs(c[3]) + b.margin(k);
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = std::min(lo[a], c[a] - R);
+      hi[a] = std::max(hi[a], c[a] + R);
+    }
+  }
+  double e[3], vol = 1;
+  for (int a = 0; a < 3; ++a) {
+    e[a] = std::max(hi[a] - lo[a], 1e-6 * (1 + std::fabs(lo[a])));
+    vol *= e[a];
+  }
+  const double cell = std::cbrt(vol / (per_sphere * double(small.size())));
+  int64_t total = 1;
+  for (int a = 0; a < 3; ++a) {
+    out.desc.n[a] = int32_t(std::min<double>(128, std::max<double>(1, std::ceil(e[a] / cell))));
+    total *= out.desc.n[a];
+  }
+  if (total > 16384) return false;
+  for (int a = 0; a < 3; ++a) {
+    // origin rounded down, cell size rounded up: the float cells cover the box
+    float g0 = float(lo[a]);
+    if (double(g0) > lo[a]) g0 = std::nextafter(g0, -INFINITY);
+    float h = float(e[a] / out.desc.n[a]);
+    while (double(g0) + double(h) * out.desc.n[a] < hi[a]) h = std::nextafter(h, INFINITY);
+    out.desc.g0[a] = g0;
+    out.desc.h[a] = h;
+    out.desc.inv_h[a] = 1.0f / h;
+    out.desc.g1[a] = std::fmaf(float(out.desc.n[a]), h, g0);
+  }
+  out.desc.ncells = int32_t(total);
+  std::vector<std::vector<uint16_t>> lists(static_cast<size_t>(total));
+  for (size_t s = 0; s < small.size(); ++s) {
+    const int32_t k = small[s];
+    const double *c = b.cr + 4 * k, R = std::fabs(c[3]) + b.margin(k);
+    int c0[3], c1[3];
+    for (int a = 0; a < 3; ++a) {
+      // cell c spans [g0 + c*h, g0 + (c+1)*h]: every cell the grown box touches
+      const double g0 = out.desc.g0[a], h = out.desc.h[a];
+      c0[a] = std::max(0, std::min(out.desc.n[a] - 1, int(std::floor((c[a] - R - g0) / h))));
+      c1[a] = std::max(0, std::min(out.desc.n[a] - 1, int(std::floor((c[a] + R - g0) / h))));
+    }
+    for (int z = c0[2]; z <= c1[2]; ++z)
+      for (int y = c0[1]; y <= c1[1]; ++y)
+        for (int x = c0[0]; x <= c1[0]; ++x)
+          lists[size_t(x + out.desc.n[0] * (y + out.desc.n[1] * z))].push_back(uint16_t(s));
+    out.sph.push_back(b.g[k]);
+    out.idx.push_back(k);
+  }
+  out.cell_start.resize(size_t(total) + 1);
+  for (int64_t cidx = 0; cidx < total; ++cidx) {
+    out.cell_start[size_t(cidx)] = uint16_t(out.refs.size());
+    out.refs.insert(out.refs.end(), lists[size_t(cidx)].begin(), lists[size_t(cidx)].end());
+    if (out.refs.size() > 65535) return false;
+  }
+  out.cell_start[size_t(total)] = uint16_t(out.refs.size());
+  out.desc.nrefs = int32_t(out.refs.size());
+  return grid_lds_bytes(int32_t(out.sph.size()), out.desc.ncells, out.desc.nrefs) <= kBvhLdsMax;
+}
+}  // namespace
+
 RTMI_EXPORT int rt_ctx_set_ordering(rt_ctx *ctx, int32_t ordering) {
   if (!ctx) return set_error(RT_EINVAL, "null ctx");
   if (ordering != RT_ORDER_NONE && ordering != RT_ORDER_COST) return set_error(RT_EINVAL, "unknown ordering %d", ordering);
@@ -1066,7 +1172,8 @@ RTMI_EXPORT int rt_ctx_set_ordering(rt_ctx *ctx, int32_t ordering) {
 
 RTMI_EXPORT int rt_ctx_set_accel(rt_ctx *ctx, int32_t accel) {
   if (!ctx) return set_error(RT_EINVAL, "null ctx");
-  if (accel != RT_ACCEL_NONE && accel != RT_ACCEL_BVH) return set_error(RT_EINVAL, "unknown accel %d", accel);
+  if (accel != RT_ACCEL_NONE && accel != RT_ACCEL_BVH && accel != RT_ACCEL_GRID)
+    return set_error(RT_EINVAL, "unknown accel %d", accel);
   ctx->accel = accel;
   return RT_OK;
 }
@@ -1184,8 +1291,42 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     ctx->resident_blocks_bvh = std::max(1, per_cu) * cus;
+    // uniform grid over the same small spheres
+    ctx->grid_ok = false;
+    GridBuild gb;
+    if (!small.empty() && n <= 65535 && build_grid(b, small, gb)) {
+      if ((rc = dev_alloc(&ctx->grid_sph, gb.sph.size())) || (rc = dev_alloc(&ctx->grid_idx, gb.idx.size())) ||
+          (rc = dev_alloc(&ctx->grid_cell_start, gb.cell_start.size())) ||
+          (rc = dev_alloc(&ctx->grid_refs, std::max<size_t>(gb.refs.size(), 1))))
+        return rc;
+      HIP_TRY(hipMemcpy(ctx->grid_sph, gb.sph.data(), gb.sph.size() * sizeof(float4), hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(ctx->grid_idx, gb.idx.data(), gb.idx.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(ctx->grid_cell_start, gb.cell_start.data(), gb.cell_start.size() * sizeof(uint16_t),
+                        hipMemcpyHostToDevice));
+      if (!gb.refs.empty())
+        HIP_TRY(hipMemcpy(ctx->grid_refs, gb.refs.data(), gb.refs.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+      ctx->grid = gb.desc;
+      ctx->grid.cell_start = ctx->grid_cell_start;
+      ctx->grid.refs = ctx->grid_refs;
+      ctx->ngrid_sph = int32_t(gb.sph.size());
+      ctx->grid_ok = true;
+      const size_t glds = grid_lds_bytes(ctx->ngrid_sph, ctx->grid.ncells, ctx->grid.nrefs);
+      per_cu = 0;
+      HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<8, true, 2>,
+                                                           64 * kWavesPerBlock, glds));
+      ctx->resident_blocks_grid = std::max(1, per_cu) * cus;
+    }
   }
   ctx->n = n;
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_ctx_grid_info(rt_ctx *ctx, int32_t *dims3, int32_t *n_refs, int32_t *lds_bytes) {
+  if (!ctx) return set_error(RT_EINVAL, "null ctx");
+  if (!ctx->grid_ok) return set_error(RT_EUNSUPPORTED, "no grid for this scene");
+  if (dims3) for (int a = 0; a < 3; ++a) dims3[a] = ctx->grid.n[a];
+  if (n_refs) *n_refs = ctx->grid.nrefs;
+  if (lds_bytes) *lds_bytes = int32_t(grid_lds_bytes(ctx->ngrid_sph, ctx->grid.ncells, ctx->grid.nrefs));
   return RT_OK;
 }
 
@@ -1230,39 +1371,65 @@ RTMI_EXPORT int rt_ctx_set_tuning(rt_ctx *ctx, int32_t tile_w, int32_t chunk) {
 
 namespace {
 
-template <int TW, bool BVH>
+size_t accel_lds_bytes(const Accel &acc, int kind) {
+  if (kind == 1) return bvh_lds_bytes(acc.nnodes, acc.nsph);
+  if (kind == 2) return grid_lds_bytes(acc.nsph, acc.grid.ncells, acc.grid.nrefs);
+  return 0;
+}
+
+// The Accel view of the context's structure of `kind` (1 BVH, 2 grid).
+Accel accel_of(const rt_ctx *ctx, int kind) {
+  Accel a{ctx->big_pairs, ctx->big_idx, ctx->nbig_pairs, 0, nullptr, nullptr, nullptr, 0, GridDesc{}};
+  if (kind == 1) {
+    a.nnodes = ctx->nnodes;
+    a.nodes = ctx->nodes;
+    a.sph = ctx->bvh_sph;
+    a.sph_idx = ctx->bvh_idx;
+    a.nsph = ctx->nbvh_sph;
+  } else if (kind == 2) {
+    a.sph = ctx->grid_sph;
+    a.sph_idx = ctx->grid_idx;
+    a.nsph = ctx->ngrid_sph;
+    a.grid = ctx->grid;
+  }
+  return a;
+}
+
+template <int TW, int ACC>
 void launch_persistent(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a,
                        unsigned long long *accum, float *out) {
-  const size_t lds = BVH ? bvh_lds_bytes(a.acc.nnodes, a.acc.nsph) : 0;
+  const size_t lds = accel_lds_bytes(a.acc, ACC);
   if (chunked)
-    hipLaunchKernelGGL((render_persistent<TW, true, BVH>), grid, dim3(64 * kWavesPerBlock), lds, st, ctx->geom, ctx->sh0,
+    hipLaunchKernelGGL((render_persistent<TW, true, ACC>), grid, dim3(64 * kWavesPerBlock), lds, st, ctx->geom, ctx->sh0,
                        ctx->sh1, ctx->pairs, a, accum, out, ctx->segments, ctx->counter);
   else
-    hipLaunchKernelGGL((render_persistent<TW, false, BVH>), grid, dim3(64 * kWavesPerBlock), lds, st, ctx->geom,
+    hipLaunchKernelGGL((render_persistent<TW, false, ACC>), grid, dim3(64 * kWavesPerBlock), lds, st, ctx->geom,
                        ctx->sh0, ctx->sh1, ctx->pairs, a, accum, out, ctx->segments, ctx->counter);
 }
 
-template <int TW, bool BVH>
+template <int TW, int ACC>
 void launch_tw(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a,
                unsigned long long *accum, float *out) {
-  const size_t lds = BVH ? bvh_lds_bytes(a.acc.nnodes, a.acc.nsph) : 0;
+  const size_t lds = accel_lds_bytes(a.acc, ACC);
   if (chunked)
-    hipLaunchKernelGGL((render_kernel<TW, true, BVH>), grid, dim3(64 * GridShape<BVH>::waves), lds, st, ctx->geom, ctx->sh0,
-                       ctx->sh1, ctx->pairs, a, accum, out, ctx->segments);
+    hipLaunchKernelGGL((render_kernel<TW, true, ACC>), grid, dim3(64 * GridShape<ACC != 0>::waves), lds, st, ctx->geom,
+                       ctx->sh0, ctx->sh1, ctx->pairs, a, accum, out, ctx->segments);
   else
-    hipLaunchKernelGGL((render_kernel<TW, false, BVH>), grid, dim3(64 * GridShape<BVH>::waves), lds, st, ctx->geom, ctx->sh0,
-                       ctx->sh1, ctx->pairs, a, accum, out, ctx->segments);
+    hipLaunchKernelGGL((render_kernel<TW, false, ACC>), grid, dim3(64 * GridShape<ACC != 0>::waves), lds, st, ctx->geom,
+                       ctx->sh0, ctx->sh1, ctx->pairs, a, accum, out, ctx->segments);
 }
 
 template <int TW>
-void launch_shape(bool persistent, bool bvh, bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx,
+void launch_shape(bool persistent, int acc, bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx,
                   const RenderArgs &a, unsigned long long *accum, float *out) {
   if (persistent) {
-    if (bvh) launch_persistent<TW, true>(chunked, grid, st, ctx, a, accum, out);
-    else launch_persistent<TW, false>(chunked, grid, st, ctx, a, accum, out);
+    if (acc == 1) launch_persistent<TW, 1>(chunked, grid, st, ctx, a, accum, out);
+    else if (acc == 2) launch_persistent<TW, 2>(chunked, grid, st, ctx, a, accum, out);
+    else launch_persistent<TW, 0>(chunked, grid, st, ctx, a, accum, out);
   } else {
-    if (bvh) launch_tw<TW, true>(chunked, grid, st, ctx, a, accum, out);
-    else launch_tw<TW, false>(chunked, grid, st, ctx, a, accum, out);
+    if (acc == 1) launch_tw<TW, 1>(chunked, grid, st, ctx, a, accum, out);
+    else if (acc == 2) launch_tw<TW, 2>(chunked, grid, st, ctx, a, accum, out);
+    else launch_tw<TW, 0>(chunked, grid, st, ctx, a, accum, out);
   }
 }
 
@@ -1310,7 +1477,10 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   // 1/4 33.4 vs 36.5, 1/8 17.9 vs 19.3); one wave per item on a whole frame
   // (128.2 vs 130.4 ms).  Both give the same image.
   const int64_t tile_samples = tiles * int64_t(spp);
-  const bool bvh = ctx->accel == RT_ACCEL_BVH && ctx->nnodes > 0;
+  // accelerated closest hit (1 BVH, 2 grid; 0 brute force) when the scene
+  // has one; both stage their structure in LDS and use the same block shape
+  const int acc_kind = ctx->accel == RT_ACCEL_BVH && ctx->nnodes > 0 ? 1 : (ctx->accel == RT_ACCEL_GRID && ctx->grid_ok ? 2 : 0);
+  const bool bvh = acc_kind != 0;
   const bool persistent = ctx->kernel == RT_KERNEL_PERSISTENT ||
                           (ctx->kernel == RT_KERNEL_AUTO && !bvh && tile_samples < 6000000);
   int32_t chunk1 = ctx->chunk, chunk2 = ctx->tail_chunk, tail = ctx->tail_spp;
@@ -1361,7 +1531,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   a.block_flush = !persistent && nch2 == 0 && nch1 % grid_wpb == 0 && ctx->block_flush;
   a.block_pool = a.block_flush && ctx->block_pool;
   if (!ctx->probing) {
-    const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush, a.block_pool, persistent ? 1 : 0, bvh ? 1 : 0};
+    const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush, a.block_pool, persistent ? 1 : 0, acc_kind};
     std::copy(sched, sched + 8, ctx->last_sched);
   }
   a.s_base = s_base;
@@ -1386,12 +1556,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   if (int64_t(tiles_y) * TH < nvalid || int64_t(tiles_x) * TW < W || nch1 * int64_t(chunk1) < spp1 ||
       nch2 * int64_t(chunk2) < spp - spp1)
     return set_error(RT_EHIP, "internal: work items do not cover the image");
-  if (bvh) {
-    a.acc = Accel{ctx->big_pairs, ctx->big_idx, ctx->nbig_pairs, ctx->nnodes, ctx->nodes, ctx->bvh_sph, ctx->bvh_idx,
-                  ctx->nbvh_sph};
-  } else {
-    a.acc = Accel{nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr, 0};
-  }
+  a.acc = bvh ? accel_of(ctx, acc_kind) : Accel{nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr, 0, GridDesc{}};
   // cost-ordered dispatch: tiles sorted by the previous render's per-tile
   // world.hit counts (same layout), most expensive first, so the dispatch
   // tail is made of cheap items.  Changes the order of work only.
@@ -1452,17 +1617,18 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     // a resident grid of waves pulling items from a global counter
     HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
     const int64_t waves =
-        std::min<int64_t>(items, int64_t(bvh ? ctx->resident_blocks_bvh : ctx->resident_blocks) * kWavesPerBlock);
+        std::min<int64_t>(items, int64_t(acc_kind == 1 ? ctx->resident_blocks_bvh
+                                         : acc_kind == 2 ? ctx->resident_blocks_grid : ctx->resident_blocks) * kWavesPerBlock);
     grid = dim3(unsigned((waves + kWavesPerBlock - 1) / kWavesPerBlock));
   } else {
     const int64_t wpb = bvh ? GridShape<true>::waves : GridShape<false>::waves;
     grid = dim3(unsigned((items + wpb - 1) / wpb));
   }
   switch (TW) {
-    case 8: launch_shape<8>(persistent, bvh, chunked, grid, st, ctx, a, accum, strip); break;
-    case 16: launch_shape<16>(persistent, bvh, chunked, grid, st, ctx, a, accum, strip); break;
-    case 32: launch_shape<32>(persistent, bvh, chunked, grid, st, ctx, a, accum, strip); break;
-    default: launch_shape<64>(persistent, bvh, chunked, grid, st, ctx, a, accum, strip); break;
+    case 8: launch_shape<8>(persistent, acc_kind, chunked, grid, st, ctx, a, accum, strip); break;
+    case 16: launch_shape<16>(persistent, acc_kind, chunked, grid, st, ctx, a, accum, strip); break;
+    case 32: launch_shape<32>(persistent, acc_kind, chunked, grid, st, ctx, a, accum, strip); break;
+    default: launch_shape<64>(persistent, acc_kind, chunked, grid, st, ctx, a, accum, strip); break;
   }
   HIP_TRY(hipGetLastError());
   if (chunked && !pass_accum) {
@@ -1782,9 +1948,10 @@ RTMI_EXPORT int rt_ctx_debug_trace(rt_ctx *ctx, uint64_t *out, int32_t cap) {
 #endif
 }
 
-// Validation: brute-force and BVH closest hits of n rays (host arrays):
-// rays[6n] = o.xyz d.xyz; idx[2n] = {brute, bvh} sphere index (-1 miss);
-// t[2n] likewise.  Not part of the render path.
+// Validation: brute-force and accelerated closest hits of n rays (host
+// arrays): rays[6n] = o.xyz d.xyz; idx[2n] = {brute, accelerated} sphere
+// index (-1 miss); t[2n] likewise.  The accelerated search is the context's
+// RT_ACCEL_GRID when selected, else the BVH.  Not part of the render path.
 RTMI_EXPORT int rt_ctx_debug_hits(rt_ctx *ctx, const float *rays, int32_t n, int32_t *idx, float *t) {
   if (!ctx || !rays || !idx || !t || n < 0) return set_error(RT_EINVAL, "rt_ctx_debug_hits: bad argument");
   if (n == 0) return RT_OK;
@@ -1797,11 +1964,19 @@ RTMI_EXPORT int rt_ctx_debug_hits(rt_ctx *ctx, const float *rays, int32_t n, int
       (rc = dev_alloc(&d_t, size_t(n) * 2)))
     return rc;
   HIP_TRY(hipMemcpy(d_rays, rays, size_t(n) * 6 * sizeof(float), hipMemcpyHostToDevice));
-  const Accel acc{ctx->big_pairs, ctx->big_idx, ctx->nbig_pairs, ctx->nnodes, ctx->nodes, ctx->bvh_sph, ctx->bvh_idx,
-                  ctx->nbvh_sph};
-  const size_t lds = ctx->nnodes ? bvh_lds_bytes(ctx->nnodes, ctx->nbvh_sph) : 0;
-  hipLaunchKernelGGL(debug_hit_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), lds, ctx->stream, ctx->pairs,
-                     ctx->npairs, acc, d_rays, n, d_idx, d_t);
+  const int kind = ctx->accel == RT_ACCEL_GRID ? 2 : 1;
+  if ((kind == 1 && !ctx->nnodes) || (kind == 2 && !ctx->grid_ok)) {
+    (void)hipFree(d_rays); (void)hipFree(d_idx); (void)hipFree(d_t);
+    return set_error(RT_EUNSUPPORTED, "rt_ctx_debug_hits: no %s for this scene", kind == 2 ? "grid" : "BVH");
+  }
+  const Accel acc = accel_of(ctx, kind);
+  const size_t lds = accel_lds_bytes(acc, kind);
+  if (kind == 1)
+    hipLaunchKernelGGL(debug_hit_kernel<1>, dim3(unsigned((n + 255) / 256)), dim3(256), lds, ctx->stream, ctx->pairs,
+                       ctx->npairs, acc, d_rays, n, d_idx, d_t);
+  else
+    hipLaunchKernelGGL(debug_hit_kernel<2>, dim3(unsigned((n + 255) / 256)), dim3(256), lds, ctx->stream, ctx->pairs,
+                       ctx->npairs, acc, d_rays, n, d_idx, d_t);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   HIP_TRY(hipMemcpy(idx, d_idx, size_t(n) * 2 * sizeof(int32_t), hipMemcpyDeviceToHost));

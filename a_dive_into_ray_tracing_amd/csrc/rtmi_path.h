@@ -607,15 +607,28 @@ constexpr int kLeafMax = RTMI_BVH_LEAF;
 constexpr int kBigGroup = RTMI_BIG_GROUP;  // sphere pairs per step of the big-sphere loop
 static_assert(kLeafMax >= 1 && kLeafMax <= 15, "leaf size");
 
+// Uniform grid over the small spheres (RT_ACCEL_GRID): cells
+// of size h over the box g0 + [0, n*h) of the spheres' margin-grown boxes;
+// cell c lists (refs[cell_start[c]] .. refs[cell_start[c+1]]) every sphere
+// whose grown box overlaps it, as 16-bit slots into the grid's sphere array.
+struct GridDesc {
+  float g0[3], h[3], inv_h[3], g1[3];  // origin, cell size, 1/h, far corner
+  int32_t n[3];
+  int32_t ncells, nrefs;
+  const uint16_t *cell_start;  // ncells + 1
+  const uint16_t *refs;
+};
+
 struct Accel {
   const SpherePair *big;     // packed pairs of the big spheres (padded like the scene)
   const int32_t *big_idx;    // scene index of each big sphere slot (2 per pair)
   int32_t nbig_pairs;
   int32_t nnodes;
   const BvhNode *nodes;
-  const float4 *sph;         // BVH spheres in leaf order: {cx, cy, cz, S}
+  const float4 *sph;         // BVH spheres in leaf order / grid spheres: {cx, cy, cz, S}
   const int32_t *sph_idx;    // their scene indices
   int32_t nsph;
+  GridDesc grid;             // RT_ACCEL_GRID only
 };
 
 // The BVH lives in LDS during a launch (dynamic shared memory, staged by
@@ -635,6 +648,192 @@ __device__ __forceinline__ void stage_bvh(const Accel &g) {
   uint16_t *idx = reinterpret_cast<uint16_t *>(rtmi_bvh_lds + g.nnodes + g.nsph);
   for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) idx[i] = uint16_t(g.sph_idx[i]);
   __syncthreads();
+}
+
+// Grid LDS layout: nsph sphere float4s, then ncells + 1 uint16 cell starts,
+// nrefs uint16 refs, nsph uint16 scene indices (scenes of < 65536 spheres,
+// < 65536 refs).
+__host__ __device__ constexpr size_t grid_lds_bytes(int32_t nsph, int32_t ncells, int32_t nrefs) {
+  return (size_t(nsph) * 16 + (size_t(ncells) + 1) * 2 + size_t(nrefs) * 2 + size_t(nsph) * 2 + 15) / 16 * 16;
+}
+
+__device__ __forceinline__ void stage_grid(const Accel &g) {
+  for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) rtmi_bvh_lds[i] = g.sph[i];
+  uint16_t *u = reinterpret_cast<uint16_t *>(rtmi_bvh_lds + g.nsph);
+  const int nstart = g.grid.ncells + 1;
+  for (int i = threadIdx.x; i < nstart; i += blockDim.x) u[i] = g.grid.cell_start[i];
+  for (int i = threadIdx.x; i < g.grid.nrefs; i += blockDim.x) u[nstart + i] = g.grid.refs[i];
+  for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) u[nstart + g.grid.nrefs + i] = uint16_t(g.sph_idx[i]);
+  __syncthreads();
+}
+
+// The ray terms of the expanded sphere test and the root logic shared by the
+// BVH and grid walks (sphere.h:21-55 restated as in hit_world_packed).
+struct RayTerms {
+  float a, inv_a, K, aL, mx, my, mz;
+  float t_max;
+  int32_t best;
+  __device__ __forceinline__ RayTerms(V3<float> o, V3<float> d) {
+    a = dot<true>(d, d);
+    inv_a = 1.0f / a;
+    K = dot<true>(o, d);
+    aL = a * dot<true>(o, o);
+    const float n2a = -2.0f * a;
+    mx = n2a * o.x; my = n2a * o.y; mz = n2a * o.z;
+    t_max = INFINITY;
+    best = -1;
+  }
+  // sphere.h:30-38 root logic; tie rule order-independent (a root equal to
+  // t_max replaces the hit only for a larger scene index)
+  __device__ __forceinline__ void resolve(int32_t idx, float hb, float disc) {
+    const float t_min = 0.001f;
+    const float sq = dsqrt(disc);
+    float root = (-hb - sq) * inv_a;
+    bool ok = !(root < t_min) && (root < t_max || (root == t_max && idx > best));
+    if (!ok) {
+      root = (-hb + sq) * inv_a;
+      ok = !(root < t_min) && (root < t_max || (root == t_max && idx > best));
+    }
+    if (ok) {
+      t_max = root;
+      best = idx;
+    }
+  }
+  // one sphere {c, S} of the expanded form: disc (< 0: no candidate) and hb
+  __device__ __forceinline__ float disc(float4 s, V3<float> d, float &hb) const {
+    hb = __builtin_fmaf(-s.x, d.x, __builtin_fmaf(-s.y, d.y, __builtin_fmaf(-s.z, d.z, K)));
+    const float acc = __builtin_fmaf(mx, s.x, __builtin_fmaf(my, s.y, __builtin_fmaf(mz, s.z, __builtin_fmaf(a, s.w, aL))));
+    return __builtin_fmaf(hb, hb, -acc);
+  }
+  // the big spheres: the packed brute-force loop (v_pk_fma_f32 over pairs)
+  template <int GP>
+  __device__ __forceinline__ void big_spheres(const Accel &acc_s, V3<float> d) {
+    const f2v DX = {d.x, d.x}, DY = {d.y, d.y}, DZ = {d.z, d.z}, KK = {K, K};
+    const f2v MX = {mx, mx}, MY = {my, my}, MZ = {mz, mz};
+    const f2v AA = {a, a}, AL = {aL, aL};
+    for (int32_t q = 0; q < acc_s.nbig_pairs; q += GP) {
+      SpherePair p[GP];
+#pragma unroll
+      for (int g = 0; g < GP; ++g) p[g] = acc_s.big[q + g];
+      f2v hb[GP], dc[GP];
+      int ci[2 * GP];
+      int any = 0;
+#pragma unroll
+      for (int g = 0; g < GP; ++g) {
+        const f2v hz = __builtin_elementwise_fma(-p[g].cz, DZ, KK);
+        hb[g] = __builtin_elementwise_fma(-p[g].cx, DX, __builtin_elementwise_fma(-p[g].cy, DY, hz));
+        const f2v ac = __builtin_elementwise_fma(MX, p[g].cx, __builtin_elementwise_fma(MY, p[g].cy,
+                       __builtin_elementwise_fma(MZ, p[g].cz, __builtin_elementwise_fma(AA, p[g].S, AL))));
+        dc[g] = __builtin_elementwise_fma(hb[g], hb[g], -ac);
+        ci[2 * g] = ~__float_as_int(dc[g].x);
+        ci[2 * g + 1] = ~__float_as_int(dc[g].y);
+        any |= ci[2 * g] | ci[2 * g + 1];
+      }
+      if (any < 0) {
+#pragma unroll
+        for (int g = 0; g < GP; ++g) {
+          if (ci[2 * g] < 0) resolve(acc_s.big_idx[2 * (q + g)], hb[g].x, dc[g].x);
+          if (ci[2 * g + 1] < 0) resolve(acc_s.big_idx[2 * (q + g) + 1], hb[g].y, dc[g].y);
+        }
+      }
+    }
+  }
+};
+
+// Inverse direction with |d_i| clamped to >= 1e-20 (see hit_world_bvh)
+__device__ __forceinline__ float safe_inv(float v) {
+  return 1.0f / (__builtin_fabsf(v) < 1e-20f ? __builtin_copysignf(1e-20f, v) : v);
+}
+
+// Closest hit through the uniform grid (RT_ACCEL_GRID, staged in LDS by
+// stage_grid): the big spheres brute force, then a 3D-DDA walk over the
+// cells the ray crosses inside [entry, t_max], testing each cell's spheres
+// with exactly the brute-force arithmetic and the order-independent tie rule.
+// The walk stops at the first cell whose exit lies at or beyond the closest
+// hit so far.  Exact: every sphere is listed in every cell
+// its grown box overlaps, the grow margin (>= 1e-3 of the sphere's scale) is
+// orders of magnitude above the float error of the cell boundaries (each
+// computed directly from the cell index, never accumulated), so the cell the
+// DDA holds for any accepted hit point lists that sphere; a sphere tested in
+// several cells gives the same root each time.
+template <int GP>
+__device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> o, V3<float> d, float &t_hit
+#if RTMI_STATS
+                                                  , unsigned *gstats
+#endif
+                                                  ) {
+  RayTerms r(o, d);
+  r.big_spheres<GP>(acc_s, d);
+  const GridDesc &G = acc_s.grid;
+  const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
+  const float ox = -o.x * ix, oy = -o.y * iy, oz = -o.z * iz;
+  // the grid box, clipped to [0, t_max]
+  const float bx0 = __builtin_fmaf(G.g0[0], ix, ox), bx1 = __builtin_fmaf(G.g1[0], ix, ox);
+  const float by0 = __builtin_fmaf(G.g0[1], iy, oy), by1 = __builtin_fmaf(G.g1[1], iy, oy);
+  const float bz0 = __builtin_fmaf(G.g0[2], iz, oz), bz1 = __builtin_fmaf(G.g1[2], iz, oz);
+  const float tnear = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(bx0, bx1), __builtin_fminf(by0, by1)),
+                                      __builtin_fmaxf(__builtin_fminf(bz0, bz1), 0.0f));
+  const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(bx0, bx1), __builtin_fmaxf(by0, by1)),
+                                     __builtin_fminf(__builtin_fmaxf(bz0, bz1), r.t_max));
+  if (tnear <= tfar) {
+    const float4 *lds_sph = rtmi_bvh_lds;
+    const uint16_t *cs = reinterpret_cast<const uint16_t *>(rtmi_bvh_lds + acc_s.nsph);
+    const uint16_t *refs = cs + G.ncells + 1;
+    const uint16_t *sidx = refs + G.nrefs;
+    // entry cell: the cell of o + tnear*d, clamped into the grid
+    auto cell_of = [&](float p, int ax) {
+      const int c = int(__builtin_floorf((p - G.g0[ax]) * G.inv_h[ax]));
+      return c < 0 ? 0 : (c >= G.n[ax] ? G.n[ax] - 1 : c);
+    };
+    int cx = cell_of(__builtin_fmaf(tnear, d.x, o.x), 0);
+    int cy = cell_of(__builtin_fmaf(tnear, d.y, o.y), 1);
+    int cz = cell_of(__builtin_fmaf(tnear, d.z, o.z), 2);
+    const int sx = d.x >= 0.0f ? 1 : -1, sy = d.y >= 0.0f ? 1 : -1, sz = d.z >= 0.0f ? 1 : -1;
+    // parameter of the far face of the current cell on each axis
+    auto tface = [&](int c, int s, int ax, float inv, float oo) {
+      return __builtin_fmaf(__builtin_fmaf(float(c + (s > 0)), G.h[ax], G.g0[ax]), inv, oo);
+    };
+    float tnx = tface(cx, sx, 0, ix, ox), tny = tface(cy, sy, 1, iy, oy), tnz = tface(cz, sz, 2, iz, oz);
+    int cell = cx + G.n[0] * (cy + G.n[1] * cz);
+    const int dcx = sx, dcy = sy * G.n[0], dcz = sz * G.n[0] * G.n[1];
+    for (;;) {
+#if RTMI_STATS
+      gstats[0] += 1;
+      if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[2] += 1;
+#endif
+      const int e = cs[cell + 1];
+      for (int k = cs[cell]; k < e; ++k) {
+#if RTMI_STATS
+        gstats[1] += 1;
+        if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[3] += 1;
+#endif
+        const int slot = refs[k];
+        float hb;
+        const float disc = r.disc(lds_sph[slot], d, hb);
+        if (!(disc < 0.0f)) r.resolve(int32_t(sidx[slot]), hb, disc);
+      }
+      const float texit = __builtin_fminf(tnx, __builtin_fminf(tny, tnz));
+      if (!(texit < r.t_max)) break;  // the closest hit so far lies in the cells walked
+      if (tnx <= tny && tnx <= tnz) {
+        cx += sx;
+        if (unsigned(cx) >= unsigned(G.n[0])) break;
+        cell += dcx;
+        tnx = tface(cx, sx, 0, ix, ox);
+      } else if (tny <= tnz) {
+        cy += sy;
+        if (unsigned(cy) >= unsigned(G.n[1])) break;
+        cell += dcy;
+        tny = tface(cy, sy, 1, iy, oy);
+      } else {
+        cz += sz;
+        if (unsigned(cz) >= unsigned(G.n[2])) break;
+        cell += dcz;
+        tnz = tface(cz, sz, 2, iz, oz);
+      }
+    }
+  }
+  t_hit = r.t_max;
+  return r.best;
 }
 
 template <int GP>

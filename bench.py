@@ -64,6 +64,7 @@ sys.path.insert(0, REPO)
 W, H, SPP, DEPTH, SEED = 1200, 800, 500, 50, 1984
 FLOP_PER_SPHERE_TEST = 18  # oc 3, hb 5, |oc|^2-r^2 7, disc 3
 FLOP_PER_NODE_TEST = 25  # slab test as executed: 6 FMA (12) + 12 min/max + 1 compare
+FLOP_PER_CELL_STEP = 5  # grid DDA step: min of 3 face parameters (2) + compare (1) + the next face's fma (2)
 PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector (MI355X_MICROARCH.md)
 PUBLISHED_CPU_MSPS = 0.1189  # README.md:16-19: rt_in_one_weekend, 1200x800x500, 16 threads, 4036.1 s
 METRIC = "Msamples/sec (pixels x spp) on RTIOW final scene"
@@ -181,10 +182,15 @@ def executed_counts(Wc, Hc, S, row0, row_step, nrows, accel="bvh"):
         return None, f"stats child failed: {e}"
 
 
-def executed_flop(c):
-    """Executed algorithmic FLOP of one BVH launch from the stats counters."""
-    return (c["node_visits"] * FLOP_PER_NODE_TEST
-            + (c["leaf_sphere_tests"] + c["segments"] * c["big_spheres"]) * FLOP_PER_SPHERE_TEST)
+def executed_flop(c, accel="bvh"):
+    """Executed algorithmic FLOP of one BVH / grid launch from the stats
+    counters ("node_visits" / "leaf_sphere_tests" count grid cells / cell
+    sphere tests for the grid, whose every segment also clips the ray to the
+    grid box: one slab test)."""
+    spheres = (c["leaf_sphere_tests"] + c["segments"] * c["big_spheres"]) * FLOP_PER_SPHERE_TEST
+    if accel == "grid":
+        return c["segments"] * FLOP_PER_NODE_TEST + c["node_visits"] * FLOP_PER_CELL_STEP + spheres
+    return c["node_visits"] * FLOP_PER_NODE_TEST + spheres
 
 
 # ------------------------------------------------------------ CPU baseline ----
@@ -326,8 +332,8 @@ def main():
     ap.add_argument("--tail-spp", type=int, default=-1)
     ap.add_argument("--tail-chunk", type=int, default=0)
     ap.add_argument("--kernel", choices=["auto", "persistent", "grid"], default="auto")
-    ap.add_argument("--accel", choices=["none", "bvh"], default="bvh",
-                    help="closest-hit search: bvh (default; same image bit for bit) or brute force")
+    ap.add_argument("--accel", choices=["none", "bvh", "grid"], default="bvh",
+                    help="closest-hit search: bvh (default), grid (uniform grid + DDA) or brute force; same image bit for bit")
     ap.add_argument("--ordering", choices=["cost", "none"], default="cost")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-exec-counts", action="store_true", help="skip the RTMI_STATS work count (roofline.frac null)")
@@ -482,7 +488,7 @@ def main():
             flop_exec, why = None, "skipped (--no-exec-counts)"
         else:
             counts, why = executed_counts(W, H, SPP, row0, row_step, nrows, args.accel)
-            flop_exec = executed_flop(counts) if counts else None
+            flop_exec = executed_flop(counts, args.accel) if counts else None
             if counts and counts["segments"] != segs:
                 why = f"stats build segments {counts['segments']} != product {segs}"
                 flop_exec = None
@@ -502,9 +508,11 @@ def main():
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_FP32_TFLOPS, 4) if achieved else None,
             "traffic": traffic,
-            "work": ("executed: node slab tests x 25 + sphere miss tests x 18 FLOP, counted per lane by the "
-                     "RTMI_STATS build on the same rows" if args.accel != "none" else
-                     "executed: segments x spheres x 18 FLOP (brute force)"),
+            "work": {"bvh": "executed: node slab tests x 25 + sphere miss tests x 18 FLOP, counted per lane by the "
+                            "RTMI_STATS build on the same rows",
+                     "grid": "executed: one grid-box slab test x 25 per segment + DDA cell steps x 5 + sphere miss "
+                             "tests x 18 FLOP, counted per lane by the RTMI_STATS build on the same rows",
+                     "none": "executed: segments x spheres x 18 FLOP (brute force)"}[args.accel],
             "flop_per_launch": flop_exec,
             "kernel_ms": round(kernel_ms, 3),
             "kernel_ms_max_rank": round(kernel_ms_max, 3),

@@ -145,8 +145,13 @@ int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind);
  * spheres much larger than the median (the ground) brute force, the rest
  * through a BVH with conservative boxes and an order-independent tie rule:
  * the same closest hit, bit for bit.  rt_ctx_accel_info
- * reports the split (big spheres, BVH nodes) of the current scene. */
-enum { RT_ACCEL_NONE = 0, RT_ACCEL_BVH = 1 };
+ * reports the split (big spheres, BVH nodes) of the current scene.
+ * RT_ACCEL_GRID: the same split, the small spheres in a uniform grid walked
+ * by a 3D DDA; same closest hit bit for bit.
+ * rt_ctx_grid_info reports its cells per axis, references and LDS bytes
+ * (RT_EUNSUPPORTED when the scene has no grid: the render then uses brute
+ * force). */
+enum { RT_ACCEL_NONE = 0, RT_ACCEL_BVH = 1, RT_ACCEL_GRID = 2 };
 
 /* Dispatch order.  RT_ORDER_COST (default): every render counts world.hit
  * calls per tile and dispatches its tiles most-expensive-first (a GPU radix
@@ -159,6 +164,7 @@ enum { RT_ORDER_NONE = 0, RT_ORDER_COST = 1 };
 int rt_ctx_set_ordering(rt_ctx *ctx, int32_t ordering);
 int rt_ctx_set_accel(rt_ctx *ctx, int32_t accel);
 int rt_ctx_accel_info(rt_ctx *ctx, int32_t *n_big, int32_t *n_nodes);
+int rt_ctx_grid_info(rt_ctx *ctx, int32_t *dims3, int32_t *n_refs, int32_t *lds_bytes);
 
 /* The whole image: replaces the 16-thread worker() block main.cpp:313-338.
  * Synchronous; `sum` is a HOST buffer of W*H*3 floats. */

@@ -88,3 +88,4 @@ def test_socket_cpus_prefers_socket0_one_per_core():
 def test_executed_flop_counts_nodes_leaves_and_big_spheres():
     c = {"segments": 10, "node_visits": 100, "leaf_sphere_tests": 30, "big_spheres": 4}
     assert bench.executed_flop(c) == 100 * 25 + (30 + 40) * 18
+    assert bench.executed_flop(c, "grid") == 10 * 25 + 100 * 5 + (30 + 40) * 18

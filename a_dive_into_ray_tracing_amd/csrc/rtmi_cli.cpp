@@ -7,6 +7,7 @@
 //               [--depth D] [--seed N] [--gpus G] [--out FILE|-] [--p6]
 //               [--tile-w 0|8|16|32|64] [--chunk N] [--scene-file F]
 //               [--save-scene F] [--pfm F] [--pass-spp N [--checkpoint F]]
+//               [--accel grid|bvh|none]
 //
 // --gpus 1 uses rt_render on device 0; --gpus G>1 (or 0 = all) uses
 // rt_render_multi (interleaved rows + one RCCL gather).  --pass-spp renders
@@ -36,6 +37,7 @@ static int die(const char *what, int rc) {
 int main(int argc, char **argv) {
   std::string scene = "final", out = "-", scene_file, save_scene, pfm, checkpoint;
   int W = 1200, H = -1, spp = 500, depth = 50, gpus = 1, p6 = 0, tile_w = 0, chunk = 0, pass_spp = 0;
+  int accel = RT_ACCEL_GRID;  // closest-hit structure (same image for every choice)
   unsigned long long seed = 1984;
   for (int a = 1; a < argc; a++) {
     auto need = [&](const char *f) -> const char * {
@@ -58,10 +60,16 @@ int main(int argc, char **argv) {
     else if (!std::strcmp(argv[a], "--pfm")) pfm = need("--pfm");
     else if (!std::strcmp(argv[a], "--pass-spp")) pass_spp = std::atoi(need("--pass-spp"));
     else if (!std::strcmp(argv[a], "--checkpoint")) checkpoint = need("--checkpoint");
+    else if (!std::strcmp(argv[a], "--accel")) {
+      const std::string v = need("--accel");
+      accel = v == "grid" ? RT_ACCEL_GRID : v == "bvh" ? RT_ACCEL_BVH : v == "none" ? RT_ACCEL_NONE : -1;
+      if (accel < 0) { std::fprintf(stderr, "unknown --accel %s\n", v.c_str()); return 2; }
+    }
     else {
       std::fprintf(stderr, "usage: %s [--scene final|learn] [--width W] [--height H] [--spp S] [--depth D]\n"
                            "          [--seed N] [--gpus G] [--out FILE|-] [--p6] [--tile-w T] [--chunk N]\n"
-                           "          [--scene-file F] [--save-scene F] [--pfm F] [--pass-spp N [--checkpoint F]]\n",
+                           "          [--scene-file F] [--save-scene F] [--pfm F] [--pass-spp N [--checkpoint F]]\n"
+                           "          [--accel grid|bvh|none]\n",
                    argv[0]);
       return 2;
     }
@@ -112,6 +120,7 @@ int main(int argc, char **argv) {
     if ((rc = rt_ctx_create(0, &ctx))) return die("rt_ctx_create", rc);
     if ((rc = rt_ctx_set_scene(ctx, &sc))) return die("rt_ctx_set_scene", rc);
     if ((rc = rt_ctx_set_tuning(ctx, tile_w, chunk))) return die("rt_ctx_set_tuning", rc);
+    if ((rc = rt_ctx_set_accel(ctx, accel))) return die("rt_ctx_set_accel", rc);
     if ((rc = rt_accum_reset(ctx, W, H))) return die("rt_accum_reset", rc);
     int done = 0;
     if (!checkpoint.empty()) {
@@ -140,6 +149,7 @@ int main(int argc, char **argv) {
     if ((rc = rt_ctx_create(0, &ctx))) return die("rt_ctx_create", rc);
     if ((rc = rt_ctx_set_scene(ctx, &sc))) return die("rt_ctx_set_scene", rc);
     if ((rc = rt_ctx_set_tuning(ctx, tile_w, chunk))) return die("rt_ctx_set_tuning", rc);
+    if ((rc = rt_ctx_set_accel(ctx, accel))) return die("rt_ctx_set_accel", rc);
     auto t0 = std::chrono::steady_clock::now();
     if ((rc = rt_render(ctx, &cam, W, H, spp, depth, seed, sum.data()))) return die("rt_render", rc);
     seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

@@ -159,9 +159,12 @@ __device__ __forceinline__ float from_fixed(int64_t v) { return float(v) * 0x1p-
 #ifndef RTMI_BVH_WAVES
 #define RTMI_BVH_WAVES 4
 #endif
+#ifndef RTMI_ACC_PER_EU
+#define RTMI_ACC_PER_EU 8
+#endif
 template <bool BVH> struct GridShape {
   static constexpr int waves = BVH ? RTMI_BVH_WAVES : kWavesPerBlock;
-  static constexpr int per_eu = BVH ? 8 : RTMI_WAVES_PER_EU;
+  static constexpr int per_eu = BVH ? RTMI_ACC_PER_EU : RTMI_WAVES_PER_EU;
 };
 // ACC: 0 brute force, 1 BVH, 2 uniform grid (RT_ACCEL_*); the accelerated
 // kernels stage their structure in LDS and share the block shape.
@@ -816,7 +819,7 @@ struct rt_ctx {
   int32_t pass_W = 0, pass_rows = 0, pass_spp = 0;
   int32_t resident_blocks = 0;             // blocks of the persistent grid (from the occupancy query)
   // BVH, built by rt_ctx_set_scene
-  int32_t accel = RT_ACCEL_NONE;
+  int32_t accel = RT_ACCEL_GRID;  // the fastest structure (brute force when the scene has none)
   SpherePair *big_pairs = nullptr;
   int32_t *big_idx = nullptr;
   int32_t nbig_pairs = 0, nbig = 0;
@@ -1086,7 +1089,7 @@ struct BvhBuilder {
 namespace {
 // Uniform grid over the small spheres.  The box of their
 // margin-grown boxes (the BVH's margins) is cut into cells of about
-// RTMI_GRID_CELLS (default 1) cells per sphere, as near cubic as the box
+// RTMI_GRID_CELLS (default 0.3) cells per sphere, as near cubic as the box
 // allows (the final scene's thin layer of spheres: 30 x 1 x 30 cells); every
 // sphere is listed in every cell its grown box overlaps.  Cell boundaries are
 // the float values g0 + c*h the device computes, so host and device agree to
@@ -1099,7 +1102,9 @@ struct GridBuild {
 };
 bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, GridBuild &out) {
   const char *env = std::getenv("RTMI_GRID_CELLS");
-  const double per_sphere = env && std::atof(env) > 0 ? std::atof(env) : 1.0;
+  // 0.3 cells per sphere: config 2 33.3 ms (0.2: 33.3, 0.5: 33.6, 1: 34.5,
+  // 2: 35.2, 4: 38.0; profiles/r02/grid_sweep)
+  const double per_sphere = env && std::atof(env) > 0 ? std::atof(env) : 0.3;
   double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
   for (int32_t k : small) {
     const double *c = b.cr + 4 * k, R = std::fabs(c[3]) + b.margin(k);

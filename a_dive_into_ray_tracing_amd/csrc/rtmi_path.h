@@ -667,82 +667,21 @@ __device__ __forceinline__ void stage_grid(const Accel &g) {
   __syncthreads();
 }
 
-// The ray terms of the expanded sphere test and the root logic shared by the
-// BVH and grid walks (sphere.h:21-55 restated as in hit_world_packed).
-struct RayTerms {
-  float a, inv_a, K, aL, mx, my, mz;
-  float t_max;
-  int32_t best;
-  __device__ __forceinline__ RayTerms(V3<float> o, V3<float> d) {
-    a = dot<true>(d, d);
-    inv_a = 1.0f / a;
-    K = dot<true>(o, d);
-    aL = a * dot<true>(o, o);
-    const float n2a = -2.0f * a;
-    mx = n2a * o.x; my = n2a * o.y; mz = n2a * o.z;
-    t_max = INFINITY;
-    best = -1;
-  }
-  // sphere.h:30-38 root logic; tie rule order-independent (a root equal to
-  // t_max replaces the hit only for a larger scene index)
-  __device__ __forceinline__ void resolve(int32_t idx, float hb, float disc) {
-    const float t_min = 0.001f;
-    const float sq = dsqrt(disc);
-    float root = (-hb - sq) * inv_a;
-    bool ok = !(root < t_min) && (root < t_max || (root == t_max && idx > best));
-    if (!ok) {
-      root = (-hb + sq) * inv_a;
-      ok = !(root < t_min) && (root < t_max || (root == t_max && idx > best));
-    }
-    if (ok) {
-      t_max = root;
-      best = idx;
-    }
-  }
-  // one sphere {c, S} of the expanded form: disc (< 0: no candidate) and hb
-  __device__ __forceinline__ float disc(float4 s, V3<float> d, float &hb) const {
-    hb = __builtin_fmaf(-s.x, d.x, __builtin_fmaf(-s.y, d.y, __builtin_fmaf(-s.z, d.z, K)));
-    const float acc = __builtin_fmaf(mx, s.x, __builtin_fmaf(my, s.y, __builtin_fmaf(mz, s.z, __builtin_fmaf(a, s.w, aL))));
-    return __builtin_fmaf(hb, hb, -acc);
-  }
-  // the big spheres: the packed brute-force loop (v_pk_fma_f32 over pairs)
-  template <int GP>
-  __device__ __forceinline__ void big_spheres(const Accel &acc_s, V3<float> d) {
-    const f2v DX = {d.x, d.x}, DY = {d.y, d.y}, DZ = {d.z, d.z}, KK = {K, K};
-    const f2v MX = {mx, mx}, MY = {my, my}, MZ = {mz, mz};
-    const f2v AA = {a, a}, AL = {aL, aL};
-    for (int32_t q = 0; q < acc_s.nbig_pairs; q += GP) {
-      SpherePair p[GP];
-#pragma unroll
-      for (int g = 0; g < GP; ++g) p[g] = acc_s.big[q + g];
-      f2v hb[GP], dc[GP];
-      int ci[2 * GP];
-      int any = 0;
-#pragma unroll
-      for (int g = 0; g < GP; ++g) {
-        const f2v hz = __builtin_elementwise_fma(-p[g].cz, DZ, KK);
-        hb[g] = __builtin_elementwise_fma(-p[g].cx, DX, __builtin_elementwise_fma(-p[g].cy, DY, hz));
-        const f2v ac = __builtin_elementwise_fma(MX, p[g].cx, __builtin_elementwise_fma(MY, p[g].cy,
-                       __builtin_elementwise_fma(MZ, p[g].cz, __builtin_elementwise_fma(AA, p[g].S, AL))));
-        dc[g] = __builtin_elementwise_fma(hb[g], hb[g], -ac);
-        ci[2 * g] = ~__float_as_int(dc[g].x);
-        ci[2 * g + 1] = ~__float_as_int(dc[g].y);
-        any |= ci[2 * g] | ci[2 * g + 1];
-      }
-      if (any < 0) {
-#pragma unroll
-        for (int g = 0; g < GP; ++g) {
-          if (ci[2 * g] < 0) resolve(acc_s.big_idx[2 * (q + g)], hb[g].x, dc[g].x);
-          if (ci[2 * g + 1] < 0) resolve(acc_s.big_idx[2 * (q + g) + 1], hb[g].y, dc[g].y);
-        }
-      }
-    }
-  }
-};
-
-// Inverse direction with |d_i| clamped to >= 1e-20 (see hit_world_bvh)
+// Inverse direction for culling only (slab tests, grid cell faces): |d_i|
+// clamped to >= 1e-20 (see hit_world_bvh), then the hardware reciprocal
+// (v_rcp_f32, ~1 ulp) instead of a correctly rounded division: the
+// structures' margins are ~1e4 times larger than that error, and no hit
+// result depends on it (the sphere tests use the exact inv_a).
+#ifndef RTMI_FAST_RCP
+#define RTMI_FAST_RCP 1
+#endif
 __device__ __forceinline__ float safe_inv(float v) {
-  return 1.0f / (__builtin_fabsf(v) < 1e-20f ? __builtin_copysignf(1e-20f, v) : v);
+  const float c = __builtin_fabsf(v) < 1e-20f ? __builtin_copysignf(1e-20f, v) : v;
+#if RTMI_FAST_RCP
+  return __builtin_amdgcn_rcpf(c);
+#else
+  return 1.0f / c;
+#endif
 }
 
 // Closest hit through the uniform grid (RT_ACCEL_GRID, staged in LDS by
@@ -762,8 +701,63 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
                                                   , unsigned *gstats
 #endif
                                                   ) {
-  RayTerms r(o, d);
-  r.big_spheres<GP>(acc_s, d);
+  // ray terms of the expanded sphere test (as hit_world_bvh)
+  const float a = dot<true>(d, d);
+  const float inv_a = 1.0f / a;
+  const float K = dot<true>(o, d);
+  const float aL = a * dot<true>(o, o);
+  const float n2a = -2.0f * a;
+  const float mx = n2a * o.x, my = n2a * o.y, mz = n2a * o.z;
+  const float t_min = 0.001f;
+  float t_max = INFINITY;
+  int32_t best = -1;
+  // sphere.h:30-38 root logic; tie rule order-independent (as hit_world_bvh)
+  auto resolve = [&](int32_t idx, float hb, float disc) {
+    const float sq = dsqrt(disc);
+    float root = (-hb - sq) * inv_a;
+    bool ok = !(root < t_min) && (root < t_max || (root == t_max && idx > best));
+    if (!ok) {
+      root = (-hb + sq) * inv_a;
+      ok = !(root < t_min) && (root < t_max || (root == t_max && idx > best));
+    }
+    if (ok) {
+      t_max = root;
+      best = idx;
+    }
+  };
+  // 1. big spheres: the packed brute-force loop
+  {
+    const f2v DX = {d.x, d.x}, DY = {d.y, d.y}, DZ = {d.z, d.z}, KK = {K, K};
+    const f2v MX = {mx, mx}, MY = {my, my}, MZ = {mz, mz};
+    const f2v AA = {a, a}, AL = {aL, aL};
+    for (int32_t q = 0; q < acc_s.nbig_pairs; q += GP) {
+      SpherePair p[GP];
+#pragma unroll
+      for (int g = 0; g < GP; ++g) p[g] = acc_s.big[q + g];
+      f2v hb[GP], disc[GP];
+      int ci[2 * GP];
+      int any = 0;
+#pragma unroll
+      for (int g = 0; g < GP; ++g) {
+        const f2v hz = __builtin_elementwise_fma(-p[g].cz, DZ, KK);
+        hb[g] = __builtin_elementwise_fma(-p[g].cx, DX, __builtin_elementwise_fma(-p[g].cy, DY, hz));
+        const f2v ac = __builtin_elementwise_fma(MX, p[g].cx, __builtin_elementwise_fma(MY, p[g].cy,
+                       __builtin_elementwise_fma(MZ, p[g].cz, __builtin_elementwise_fma(AA, p[g].S, AL))));
+        disc[g] = __builtin_elementwise_fma(hb[g], hb[g], -ac);
+        ci[2 * g] = ~__float_as_int(disc[g].x);
+        ci[2 * g + 1] = ~__float_as_int(disc[g].y);
+        any |= ci[2 * g] | ci[2 * g + 1];
+      }
+      if (any < 0) {
+#pragma unroll
+        for (int g = 0; g < GP; ++g) {
+          if (ci[2 * g] < 0) resolve(acc_s.big_idx[2 * (q + g)], hb[g].x, disc[g].x);
+          if (ci[2 * g + 1] < 0) resolve(acc_s.big_idx[2 * (q + g) + 1], hb[g].y, disc[g].y);
+        }
+      }
+    }
+  }
+  // 2. the grid (staged in LDS by stage_grid)
   const GridDesc &G = acc_s.grid;
   const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
   const float ox = -o.x * ix, oy = -o.y * iy, oz = -o.z * iz;
@@ -774,7 +768,7 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
   const float tnear = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(bx0, bx1), __builtin_fminf(by0, by1)),
                                       __builtin_fmaxf(__builtin_fminf(bz0, bz1), 0.0f));
   const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(bx0, bx1), __builtin_fmaxf(by0, by1)),
-                                     __builtin_fminf(__builtin_fmaxf(bz0, bz1), r.t_max));
+                                     __builtin_fminf(__builtin_fmaxf(bz0, bz1), t_max));
   if (tnear <= tfar) {
     const float4 *lds_sph = rtmi_bvh_lds;
     const uint16_t *cs = reinterpret_cast<const uint16_t *>(rtmi_bvh_lds + acc_s.nsph);
@@ -808,12 +802,14 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
         if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[3] += 1;
 #endif
         const int slot = refs[k];
-        float hb;
-        const float disc = r.disc(lds_sph[slot], d, hb);
-        if (!(disc < 0.0f)) r.resolve(int32_t(sidx[slot]), hb, disc);
+        const float4 sp = lds_sph[slot];
+        const float hb = __builtin_fmaf(-sp.x, d.x, __builtin_fmaf(-sp.y, d.y, __builtin_fmaf(-sp.z, d.z, K)));
+        const float ac = __builtin_fmaf(mx, sp.x, __builtin_fmaf(my, sp.y, __builtin_fmaf(mz, sp.z, __builtin_fmaf(a, sp.w, aL))));
+        const float disc = __builtin_fmaf(hb, hb, -ac);
+        if (!(disc < 0.0f)) resolve(int32_t(sidx[slot]), hb, disc);
       }
       const float texit = __builtin_fminf(tnx, __builtin_fminf(tny, tnz));
-      if (!(texit < r.t_max)) break;  // the closest hit so far lies in the cells walked
+      if (!(texit < t_max)) break;  // the closest hit so far lies in the cells walked
       if (tnx <= tny && tnx <= tnz) {
         cx += sx;
         if (unsigned(cx) >= unsigned(G.n[0])) break;
@@ -832,8 +828,8 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
       }
     }
   }
-  t_hit = r.t_max;
-  return r.best;
+  t_hit = t_max;
+  return best;
 }
 
 template <int GP>
@@ -909,7 +905,6 @@ __device__ __forceinline__ int32_t hit_world_bvh(const Accel &acc_s, V3<float> o
   // reliably).  The clamp moves the ray by a negligible angle; a ray running
   // parallel to a slab plane within ~1e-6 of it cannot reach a sphere, which
   // sits at least the box margin inside every face.
-  auto safe_inv = [](float v) { return 1.0f / (__builtin_fabsf(v) < 1e-20f ? __builtin_copysignf(1e-20f, v) : v); };
   const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
   // slab distances as one fma per plane: (b - o) * i = fma(b, i, -o*i); the
   // box margin covers the different rounding

@@ -17,18 +17,21 @@ refuses to run when fewer than N GPUs are visible.  After the timed region
 rank 0 renders the whole frame alone and checks the gathered image against
 it bit for bit ("gather_check").
 
-Closest hits go through the BVH by default (--accel bvh): the same closest
-hit as the brute-force loop, bit for bit (tests/test_gpu_parity.py), so the
-same image.  --accel none times the brute-force kernel.
+Closest hits go through the uniform grid by default (--accel grid; --accel
+bvh the BVH): the same closest hit as the brute-force loop, bit for bit
+(tests/test_gpu_parity.py), so the same image.  --accel none times the
+brute-force kernel.
 
 roofline (FP32 VALU): `achieved` = the EXECUTED algorithmic FLOP
 of the timed kernel's launch / its mean duration (HIP events on the launch
-stream).  With the BVH the executed work is counted exactly by the
+stream).  With the grid or BVH the executed work is counted exactly by the
 RTMI_STATS build of the same kernel (librtmi_stats.so, one extra untimed
 render of the same rows in a child process; same paths, same image):
-every lane's node slab tests x 25 FLOP (6 FMA + 12 min/max + 1 compare) plus
-its sphere miss tests (leaf spheres and the brute-force big spheres) x 18
-FLOP (sphere.h:21-55).  Brute force executes segments x N x 18.
+every lane's sphere miss tests (cell / leaf spheres and the brute-force big
+spheres) x 18 FLOP (sphere.h:21-55) plus, for the grid, one
+grid-box slab test per segment x 25 (6 FMA + 12 min/max + 1 compare) and its
+DDA cell steps x 5, for the BVH its node slab tests x 25.  Brute force
+executes segments x N x 18.
 peak = 157.3 TFLOP/s FP32 vector.  `work_equivalent_*` keeps SURVEY §8(d)'s
 brute-force-equivalent figure (segments x 487 x 18 over the BVH time, which
 can exceed 1) and `brute_force_*` the brute-force kernel's own roofline from
@@ -332,8 +335,8 @@ def main():
     ap.add_argument("--tail-spp", type=int, default=-1)
     ap.add_argument("--tail-chunk", type=int, default=0)
     ap.add_argument("--kernel", choices=["auto", "persistent", "grid"], default="auto")
-    ap.add_argument("--accel", choices=["none", "bvh", "grid"], default="bvh",
-                    help="closest-hit search: bvh (default), grid (uniform grid + DDA) or brute force; same image bit for bit")
+    ap.add_argument("--accel", choices=["none", "bvh", "grid"], default="grid",
+                    help="closest-hit search: grid (default: uniform grid + DDA), bvh or brute force; same image bit for bit")
     ap.add_argument("--ordering", choices=["cost", "none"], default="cost")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-exec-counts", action="store_true", help="skip the RTMI_STATS work count (roofline.frac null)")

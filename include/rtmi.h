@@ -152,6 +152,8 @@ int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind);
  * (RT_EUNSUPPORTED when the scene has no grid: the render then uses brute
  * force). */
 enum { RT_ACCEL_NONE = 0, RT_ACCEL_BVH = 1, RT_ACCEL_GRID = 2 };
+/* (a new context starts with RT_ACCEL_GRID: same image as brute force, and
+ * the fastest on the reference's scenes — DESIGN.md §4.5) */
 
 /* Dispatch order.  RT_ORDER_COST (default): every render counts world.hit
  * calls per tile and dispatches its tiles most-expensive-first (a GPU radix

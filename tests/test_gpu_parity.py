@@ -37,6 +37,7 @@ def final_world():
 @pytest.fixture(scope="module")
 def final_renderer(final_world):
     r = rt.Renderer(final_world, 0)
+    r.set_accel("none")  # brute force unless a test selects a structure
     yield r
     r.close()
 
@@ -44,6 +45,7 @@ def final_renderer(final_world):
 @pytest.fixture(scope="module")
 def learn_renderer():
     r = rt.Renderer(rt.learn_scene(), 0)
+    r.set_accel("none")
     yield r
     r.close()
 
@@ -351,6 +353,7 @@ def test_bvh_random_scenes_equal_brute_force(seed, scale, shift, accel):
     cam = rt.camera(look_from, (shift, 0, 0), (0, 1, 0), 40.0, 1.5, 0.1 * scale, 10.0 * scale)
     r_ = rt.Renderer(world, 0)
     try:
+        r_.set_accel("none")
         want = r_.render(cam, 72, 48, 6, 50, SEED)
         r_.set_accel(accel)
         got = r_.render(cam, 72, 48, 6, 50, SEED)
@@ -564,3 +567,14 @@ def test_config5_strip_of_8_equals_frame_rows(config5, final_renderer):
     mean = float(img.mean() / S)
     record_parity_stats("config5_frame", {"mean_radiance": mean, "rows_checked_vs_oracle": "0, 1531", "strip": "3 of 8"})
     assert 0.3 < mean < 0.9
+
+
+def test_default_accel_is_grid(final_world):
+    """A new context renders through the uniform grid (the fastest structure;
+    same image as brute force): rt_render, the reference's surface, gets it."""
+    r = rt.Renderer(final_world, 0)
+    try:
+        r.render(rt.final_camera(1.5), 24, 16, 2, 50, SEED)
+        assert r.last_schedule()["bvh"] == 2
+    finally:
+        r.close()

@@ -142,6 +142,15 @@ constexpr int kPairGroup = RTMI_PAIR_GROUP;  // sphere pairs per scalar-load gro
 // sum of up to 2^24 samples cannot overflow (64 * 2^24 * 2^32 = 2^62);
 // every scene here stays far inside (RTIOW colours are <= 1).  The oracle
 // applies the identical guard.
+// q / d for 0 <= q < 2^22 and 1 <= d <= 2^16, given inv_d = 1.0f / d: the
+// float quotient is within one of the true one, fixed by one correction.
+__device__ __forceinline__ int div_small(int q, int d, float inv_d) {
+  int t = int(float(q) * inv_d);
+  const int r = q - t * d;
+  t += (r >= d ? 1 : 0) - (r < 0 ? 1 : 0);
+  return t;
+}
+
 __device__ __forceinline__ int64_t to_fixed(float c) {
   const float g = c == c ? (c > 64.0f ? 64.0f : (c < -64.0f ? -64.0f : c)) : 0.0f;
   return int64_t(g * 4294967296.0f);
@@ -235,10 +244,14 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
 
   // job q -> pixel px = q % nv, sample s0 + q / nv (sample-major, so every
   // pixel of the tile advances together); then the camera ray.
+  // q / nv and px / vw by a float reciprocal with one correction step:
+  // exact for q < 2^22 (a job index here is < 64 * spp per item)
+  const float inv_nv = 1.0f / float(max(nv, 1)), inv_vw = 1.0f / float(vw);
   auto start = [&](int q) {
-    const int s = s0 + q / nv;
-    px = q - (q / nv) * nv;
-    const int ly = px / vw, lx = px - ly * vw;
+    const int qs = div_small(q, nv, inv_nv);
+    const int s = s0 + qs;
+    px = q - qs * nv;
+    const int ly = div_small(px, vw, inv_vw), lx = px - ly * vw;
     const int i = x0 + lx;
     const int j = a.row0 + (y0 + ly) * a.row_step;
     rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(a.s_base + s));
@@ -299,7 +312,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
         V3<float> p, nrm, at, nd;
         bool front;
         hit_record<true, float>(sc, k, o, d, t, p, nrm, front);
-        if (!scatter<true, float>(sc, k, d, nrm, front, rng, at, nd)) {
+        if (!scatter_fast(sc, k, d, nrm, front, rng, at, nd)) {
           done = true;  // absorbed (metal below the surface): black, main.cpp:78
         } else {
           T = mk(T.x * at.x, T.y * at.y, T.z * at.z);
@@ -626,7 +639,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
         V3<float> p, nrm, at, nd;
         bool front;
         hit_record<true, float>(sc, k, o, d, t, p, nrm, front);
-        if (!scatter<true, float>(sc, k, d, nrm, front, rng, at, nd)) {
+        if (!scatter_fast(sc, k, d, nrm, front, rng, at, nd)) {
           done = true;
         } else {
           T = mk(T.x * at.x, T.y * at.y, T.z * at.z);

@@ -997,6 +997,69 @@ __device__ __forceinline__ bool scatter(const SceneView<R> &sc, int32_t k, V3<R>
   return true;
 }
 
+// The fast kernels' form of scatter<true, float, Xoro>: the same arithmetic
+// and random draws per lane, arranged so that the parts materials share run
+// once per wave instead of once per material branch (a wave's lanes hit all
+// three materials at once):
+//  * every material's first draw is one xoroshiro step: lambertian and metal
+//    take its (u, v) pair for unit_dir, the dielectric its top 24 bits as
+//    g.uni() — the same u;
+//  * metal and dielectric share unit(din) and reflect(unit(din), n).
+// The dielectric draws its uniform only when it can refract (the short
+// circuit of material.h:80): a dielectric lane that cannot refract gets its
+// generator state back.
+__device__ __forceinline__ bool scatter_fast(const SceneView<float> &sc, int32_t k, V3<float> din, V3<float> normal,
+                                             bool front, Xoro &g, V3<float> &atten, V3<float> &dout) {
+  const float4 s0 = sc.sh0[k];
+  const float4 s1 = sc.sh1[k];
+  const int kind = int(s1.x);
+  const Xoro g0 = g;
+  float u, v;
+  g.pair(u, v);  // the first draw of every material
+  V3<float> ud = mk(0.f, 0.f, 0.f), refl = mk(0.f, 0.f, 0.f);
+  if (kind != RT_MAT_LAMBERTIAN) {  // metal, dielectric: unit(din), reflect
+    ud = unit<true>(din);
+    refl = reflect<true>(ud, normal);
+  }
+  if (kind != RT_MAT_DIELECTRIC) {  // lambertian, metal: unit_dir from (u, v)
+    const float z = __builtin_fmaf(-2.0f, u, 1.0f);
+    const float r = __builtin_sqrtf(__builtin_fmaf(-z, z, 1.0f));
+    float c, sn;
+    sincos2pi(v, c, sn);
+    const V3<float> ru = mk(r * c, r * sn, z);
+    atten = mk(s0.y, s0.z, s0.w);
+    if (kind == RT_MAT_LAMBERTIAN) {  // material.h:19-31
+      V3<float> dir = mk(normal.x + ru.x, normal.y + ru.y, normal.z + ru.z);
+      if (near_zero(dir)) dir = normal;
+      dout = dir;
+      return true;
+    }
+    // metal material.h:40-49: a point in the ball = ru * max of three uniforms
+    float a, b, cc, unused;
+    g.pair(a, b);
+    g.pair(cc, unused);
+    const float rr = __builtin_fmaxf(a, __builtin_fmaxf(b, cc));
+    const V3<float> rv = mk(rr * ru.x, rr * ru.y, rr * ru.z);
+    const float fz = s1.y;
+    const V3<float> dir = mk(__builtin_fmaf(fz, rv.x, refl.x), __builtin_fmaf(fz, rv.y, refl.y),
+                             __builtin_fmaf(fz, rv.z, refl.z));
+    dout = dir;
+    return dot<true>(dir, normal) > 0.0f;
+  }
+  // dielectric material.h:60-85
+  atten = mk(1.f, 1.f, 1.f);
+  const float ratio = front ? s1.w : s1.z;
+  const float cos_theta = dfmin(dot<true>(mk(-ud.x, -ud.y, -ud.z), normal), 1.0f);
+  const float sin_theta = dsqrt(__builtin_fmaf(-cos_theta, cos_theta, 1.0f));
+  const bool cannot_refract = ratio * sin_theta > 1.0f;
+  if (cannot_refract) g = g0;  // the uniform is not drawn
+  if (cannot_refract || reflectance<true>(cos_theta, ratio) > u)
+    dout = refl;
+  else
+    dout = refract<true>(ud, normal, ratio, cos_theta);
+  return true;
+}
+
 // Hit record (sphere.h:43-53, hittable.h:23-26) for sphere k at t.
 template <bool F, class R>
 __device__ __forceinline__ void hit_record(const SceneView<R> &sc, int32_t k, V3<R> o, V3<R> d, R t,

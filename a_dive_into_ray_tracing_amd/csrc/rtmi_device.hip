@@ -121,6 +121,12 @@ __device__ unsigned g_trace_n;
 #ifndef RTMI_FAIR
 #define RTMI_FAIR 3
 #endif
+// the grid kernel keeps the camera in LDS (config 2: 30.1 -> 28.2 ms: the
+// scalar registers it occupied were spilled to VGPR lanes and read back
+// with v_readlane at every regeneration)
+#ifndef RTMI_CAM_LDS
+#define RTMI_CAM_LDS 1
+#endif
 // RTMI_CHECK builds (analysis only) bounds-check every accumulator write and
 // count violations in segments[5..7] instead of performing them.
 #ifndef RTMI_CHECK
@@ -187,11 +193,32 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   __shared__ unsigned long long acc[WPB][3][64];
   __shared__ unsigned long long wave_segs[WPB];
   __shared__ unsigned pool_next;  // block pool: next unclaimed job
+#if RTMI_CAM_LDS
+  // the camera in LDS, read at each regeneration: kept out of the wave's
+  // scalar registers (which spill it to VGPR lanes otherwise)
+  __shared__ float cam_lds[20];
+#endif
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * WPB + wave;
   const bool pool = CHUNKED && a.block_pool;  // block-uniform (implies block_flush)
   if (pool && threadIdx.x == 0) pool_next = 64 * WPB;
+#if RTMI_CAM_LDS
+  if (threadIdx.x < 19) {
+    float v;
+    switch (threadIdx.x / 3) {
+      case 0: v = (&a.cam.origin.x)[threadIdx.x % 3]; break;
+      case 1: v = (&a.cam.llc.x)[threadIdx.x % 3]; break;
+      case 2: v = (&a.cam.hor.x)[threadIdx.x % 3]; break;
+      case 3: v = (&a.cam.ver.x)[threadIdx.x % 3]; break;
+      case 4: v = (&a.cam.u.x)[threadIdx.x % 3]; break;
+      case 5: v = (&a.cam.v.x)[threadIdx.x % 3]; break;
+      default: v = a.cam.lens; break;
+    }
+    cam_lds[threadIdx.x] = v;
+  }
+  if constexpr (ACC == 0) __syncthreads();  // (accelerated kernels: stage_* ends with one)
+#endif
   if constexpr (ACC == 1) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
   else if constexpr (ACC == 2) stage_grid(a.acc);
   else if (pool) __syncthreads();
@@ -259,7 +286,20 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
     rng.pair(ju, jv);
     const float u = (float(i) + ju) / float(a.W - 1);  // main.cpp:278
     const float v = (float(j) + jv) / float(a.H - 1);  // main.cpp:279
+#if RTMI_CAM_LDS
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // read here, not hoisted out of the loop
+    Cam<float> cm;
+    cm.origin = mk(cam_lds[0], cam_lds[1], cam_lds[2]);
+    cm.llc = mk(cam_lds[3], cam_lds[4], cam_lds[5]);
+    cm.hor = mk(cam_lds[6], cam_lds[7], cam_lds[8]);
+    cm.ver = mk(cam_lds[9], cam_lds[10], cam_lds[11]);
+    cm.u = mk(cam_lds[12], cam_lds[13], cam_lds[14]);
+    cm.v = mk(cam_lds[15], cam_lds[16], cam_lds[17]);
+    cm.lens = cam_lds[18];
+    get_ray<true, float>(cm, u, v, rng, o, d);
+#else
     get_ray<true, float>(a.cam, u, v, rng, o, d);
+#endif
     T = mk(1.f, 1.f, 1.f);
     depth = 0;
   };
@@ -882,6 +922,10 @@ struct rt_ctx {
   // before every render (no state carried between renders)
   int32_t probe_mode = std::getenv("RTMI_ORDER_PROBE") ? std::atoi(std::getenv("RTMI_ORDER_PROBE")) : 1;
   bool probing = false;
+  // automatic item size of the grid kernel: ~want_items items of item_min..125
+  // samples (RTMI_WANT_ITEMS / RTMI_ITEM_MIN override, for A/B)
+  int64_t want_items = std::getenv("RTMI_WANT_ITEMS") ? std::atoll(std::getenv("RTMI_WANT_ITEMS")) : 60000;
+  int32_t item_min = std::getenv("RTMI_ITEM_MIN") ? std::atoi(std::getenv("RTMI_ITEM_MIN")) : 24;
 };
 
 namespace rtmi {
@@ -1176,6 +1220,20 @@ bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, GridBuil
   }
   out.cell_start[size_t(total)] = uint16_t(out.refs.size());
   out.desc.nrefs = int32_t(out.refs.size());
+#if RTMI_GRID_DIRECT
+  {  // each cell's spheres stored contiguously: sphere data per reference
+    std::vector<float4> sph;
+    std::vector<int32_t> idx;
+    for (uint16_t slot : out.refs) {
+      sph.push_back(out.sph[slot]);
+      idx.push_back(out.idx[slot]);
+    }
+    out.sph.swap(sph);
+    out.idx.swap(idx);
+    out.refs.clear();
+    out.desc.nrefs = 0;
+  }
+#endif
   return grid_lds_bytes(int32_t(out.sph.size()), out.desc.ncells, out.desc.nrefs) <= kBvhLdsMax;
 }
 }  // namespace
@@ -1513,8 +1571,8 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     // rank's 1/8 strip 8.06 ms with 7, 7.37 with 14, 7.18 with 21, 7.27 with
     // 32 (profiles/r01/session6/chunk_ab.txt): long items pay the per-item
     // ramp-down less often, short ones shorten a small grid's dispatch tail
-    const int64_t want_items = 60000;
-    chunk1 = int32_t(std::min<int64_t>(125, std::max<int64_t>(24, tile_samples / want_items)));
+    const int64_t want_items = ctx->want_items;
+    chunk1 = int32_t(std::min<int64_t>(125, std::max<int64_t>(ctx->item_min, tile_samples / want_items)));
   }
   if (chunk2 <= 0) chunk2 = std::max(1, chunk1 / 4);
   if (tail < 0) tail = 0;  // automatic: no short-item phase (it measured no better)

@@ -22,6 +22,18 @@
 #ifndef RTMI_DISC_ONLY
 #define RTMI_DISC_ONLY 1
 #endif
+#ifndef RTMI_GRID_UNROLL2
+#define RTMI_GRID_UNROLL2 0
+#endif
+// RTMI_GRID_DIRECT: the grid stores each cell's spheres contiguously (a
+// sphere listed in several cells is stored in each), so a cell-sphere test
+// reads its sphere directly instead of through a 16-bit reference
+#ifndef RTMI_GRID_DIRECT
+#define RTMI_GRID_DIRECT 0
+#endif
+#ifndef RTMI_CHEAP_SEED
+#define RTMI_CHEAP_SEED 0
+#endif
 
 namespace rtmi {
 
@@ -100,7 +112,11 @@ struct Xoro {
   uint64_t s0, s1;
   __device__ __forceinline__ void init(uint64_t seed, uint64_t pixel, uint32_t sample) {
     const uint64_t key = (pixel << 24) | uint64_t(sample);
+#if RTMI_CHEAP_SEED
+    s0 = mix64(seed ^ (key * 0x9E3779B97F4A7C15ULL));
+#else
     s0 = mix64(seed ^ mix64(key + 0x9E3779B97F4A7C15ULL));
+#endif
     s1 = mix64(s0 + 0x9E3779B97F4A7C15ULL);
   }
   __device__ __forceinline__ uint64_t next() {
@@ -796,18 +812,43 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
       if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[2] += 1;
 #endif
       const int e = cs[cell + 1];
+#if RTMI_GRID_UNROLL2
+      // two spheres of the cell per iteration (the second predicated off at
+      // an odd end): half the loop control, two independent LDS chains
+      for (int k = cs[cell]; k < e; k += 2) {
+#if RTMI_STATS
+        gstats[1] += 1 + (k + 1 < e);
+        if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[3] += 2;
+#endif
+        const bool has1 = k + 1 < e;
+        const int slot0 = refs[k], slot1 = refs[has1 ? k + 1 : k];
+        const float4 s0 = lds_sph[slot0], s1 = lds_sph[slot1];
+        const float hb0 = __builtin_fmaf(-s0.x, d.x, __builtin_fmaf(-s0.y, d.y, __builtin_fmaf(-s0.z, d.z, K)));
+        const float hb1 = __builtin_fmaf(-s1.x, d.x, __builtin_fmaf(-s1.y, d.y, __builtin_fmaf(-s1.z, d.z, K)));
+        const float ac0 = __builtin_fmaf(mx, s0.x, __builtin_fmaf(my, s0.y, __builtin_fmaf(mz, s0.z, __builtin_fmaf(a, s0.w, aL))));
+        const float ac1 = __builtin_fmaf(mx, s1.x, __builtin_fmaf(my, s1.y, __builtin_fmaf(mz, s1.z, __builtin_fmaf(a, s1.w, aL))));
+        const float disc0 = __builtin_fmaf(hb0, hb0, -ac0), disc1 = __builtin_fmaf(hb1, hb1, -ac1);
+        if (!(disc0 < 0.0f)) resolve(int32_t(sidx[slot0]), hb0, disc0);
+        if (has1 && !(disc1 < 0.0f)) resolve(int32_t(sidx[slot1]), hb1, disc1);
+      }
+#else
       for (int k = cs[cell]; k < e; ++k) {
 #if RTMI_STATS
         gstats[1] += 1;
         if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[3] += 1;
 #endif
+#if RTMI_GRID_DIRECT
+        const int slot = k;
+#else
         const int slot = refs[k];
+#endif
         const float4 sp = lds_sph[slot];
         const float hb = __builtin_fmaf(-sp.x, d.x, __builtin_fmaf(-sp.y, d.y, __builtin_fmaf(-sp.z, d.z, K)));
         const float ac = __builtin_fmaf(mx, sp.x, __builtin_fmaf(my, sp.y, __builtin_fmaf(mz, sp.z, __builtin_fmaf(a, sp.w, aL))));
         const float disc = __builtin_fmaf(hb, hb, -ac);
         if (!(disc < 0.0f)) resolve(int32_t(sidx[slot]), hb, disc);
       }
+#endif
       const float texit = __builtin_fminf(tnx, __builtin_fminf(tny, tnz));
       if (!(texit < t_max)) break;  // the closest hit so far lies in the cells walked
       if (tnx <= tny && tnx <= tnz) {

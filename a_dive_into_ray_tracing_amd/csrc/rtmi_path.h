@@ -127,12 +127,15 @@ struct Xoro {
     return r;
   }
   // top 24 bits: uniform on [0,1) exactly representable in float
-  __device__ __forceinline__ float uni() { return float(uint32_t(next() >> 40)) * 0x1p-24f; }
+  // (32-bit extraction spelled out: the compiler otherwise emits a 64-bit
+  // integer -> float conversion for some uses)
+  __device__ __forceinline__ float uni() { return float(uint32_t(next() >> 32) >> 8) * 0x1p-24f; }
   // two uniforms from one step: bits 63..40 and 39..16
   __device__ __forceinline__ void pair(float &u, float &v) {
     const uint64_t r = next();
-    u = float(uint32_t(r >> 40)) * 0x1p-24f;
-    v = float(uint32_t(r >> 16) & 0xFFFFFFu) * 0x1p-24f;
+    const uint32_t hi = uint32_t(r >> 32), lo = uint32_t(r);
+    u = float(hi >> 8) * 0x1p-24f;
+    v = float(((hi & 0xFFu) << 16) | (lo >> 16)) * 0x1p-24f;
   }
 };
 

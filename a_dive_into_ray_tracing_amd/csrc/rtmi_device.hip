@@ -344,15 +344,21 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
 #if RTMI_CHECK
       if (k >= a.n) atomicAdd(&segments[7], 1ull << 32);
 #endif
-      if (k < 0 || (RTMI_CHECK && k >= a.n)) {
-        const V3<float> sk = sky<true, float>(d);
+      // 1/|d| once for the lanes that need it: the sky of a miss (main.cpp:80)
+      // and unit(din) of metal and dielectric — the same expression
+      const bool miss = k < 0 || (RTMI_CHECK && k >= a.n);
+      const int kind = miss ? -1 : int(sc.sh1[k].x);
+      float inv_len = 0.0f;
+      if (kind != RT_MAT_LAMBERTIAN) inv_len = 1.0f / dsqrt(dot<true>(d, d));
+      if (miss) {
+        const V3<float> sk = sky_fast(d, inv_len);
         col = mk(T.x * sk.x, T.y * sk.y, T.z * sk.z);
         done = true;
       } else {
         V3<float> p, nrm, at, nd;
         bool front;
         hit_record<true, float>(sc, k, o, d, t, p, nrm, front);
-        if (!scatter_fast(sc, k, d, nrm, front, rng, at, nd)) {
+        if (!scatter_fast(sc, k, d, nrm, front, rng, at, nd, inv_len)) {
           done = true;  // absorbed (metal below the surface): black, main.cpp:78
         } else {
           T = mk(T.x * at.x, T.y * at.y, T.z * at.z);
@@ -671,15 +677,21 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
 #if RTMI_CHECK
       if (k >= a.n) atomicAdd(&segments[7], 1ull << 32);
 #endif
-      if (k < 0 || (RTMI_CHECK && k >= a.n)) {
-        const V3<float> sk = sky<true, float>(d);
+      // 1/|d| once for the lanes that need it: the sky of a miss (main.cpp:80)
+      // and unit(din) of metal and dielectric — the same expression
+      const bool miss = k < 0 || (RTMI_CHECK && k >= a.n);
+      const int kind = miss ? -1 : int(sc.sh1[k].x);
+      float inv_len = 0.0f;
+      if (kind != RT_MAT_LAMBERTIAN) inv_len = 1.0f / dsqrt(dot<true>(d, d));
+      if (miss) {
+        const V3<float> sk = sky_fast(d, inv_len);
         col = mk(T.x * sk.x, T.y * sk.y, T.z * sk.z);
         done = true;
       } else {
         V3<float> p, nrm, at, nd;
         bool front;
         hit_record<true, float>(sc, k, o, d, t, p, nrm, front);
-        if (!scatter_fast(sc, k, d, nrm, front, rng, at, nd)) {
+        if (!scatter_fast(sc, k, d, nrm, front, rng, at, nd, inv_len)) {
           done = true;
         } else {
           T = mk(T.x * at.x, T.y * at.y, T.z * at.z);

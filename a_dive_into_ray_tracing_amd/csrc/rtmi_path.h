@@ -1052,8 +1052,10 @@ __device__ __forceinline__ bool scatter(const SceneView<R> &sc, int32_t k, V3<R>
 // The dielectric draws its uniform only when it can refract (the short
 // circuit of material.h:80): a dielectric lane that cannot refract gets its
 // generator state back.
+// inv_len = 1/sqrt(din.din) (correctly rounded), as unit() computes it; the
+// caller shares it with the sky of the wave's missed lanes.
 __device__ __forceinline__ bool scatter_fast(const SceneView<float> &sc, int32_t k, V3<float> din, V3<float> normal,
-                                             bool front, Xoro &g, V3<float> &atten, V3<float> &dout) {
+                                             bool front, Xoro &g, V3<float> &atten, V3<float> &dout, float inv_len) {
   const float4 s0 = sc.sh0[k];
   const float4 s1 = sc.sh1[k];
   const int kind = int(s1.x);
@@ -1062,7 +1064,7 @@ __device__ __forceinline__ bool scatter_fast(const SceneView<float> &sc, int32_t
   g.pair(u, v);  // the first draw of every material
   V3<float> ud = mk(0.f, 0.f, 0.f), refl = mk(0.f, 0.f, 0.f);
   if (kind != RT_MAT_LAMBERTIAN) {  // metal, dielectric: unit(din), reflect
-    ud = unit<true>(din);
+    ud = scale(inv_len, din);
     refl = reflect<true>(ud, normal);
   }
   if (kind != RT_MAT_DIELECTRIC) {  // lambertian, metal: unit_dir from (u, v)
@@ -1116,7 +1118,12 @@ __device__ __forceinline__ void hit_record(const SceneView<R> &sc, int32_t k, V3
   normal = front ? outward : mk(-outward.x, -outward.y, -outward.z);
 }
 
-// sky, main.cpp:80-82
+// sky, main.cpp:80-82, given inv_len = 1/sqrt(d.d) (the fast kernels share it)
+__device__ __forceinline__ V3<float> sky_fast(V3<float> d, float inv_len) {
+  const float uy = inv_len * d.y;
+  const float t = 0.5f * (uy + 1.0f);
+  return mk(__builtin_fmaf(t, 0.5f, 1.0f - t), __builtin_fmaf(t, 0.7f, 1.0f - t), __builtin_fmaf(t, 1.0f, 1.0f - t));
+}
 template <bool F, class R> __device__ __forceinline__ V3<R> sky(V3<R> d) {
   const R uy = (R(1) / dsqrt(dot<F>(d, d))) * d.y;
   const R t = R(0.5) * (uy + R(1));

@@ -127,6 +127,9 @@ __device__ unsigned g_trace_n;
 #ifndef RTMI_CAM_LDS
 #define RTMI_CAM_LDS 1
 #endif
+#ifndef RTMI_REGEN_TWICE
+#define RTMI_REGEN_TWICE 0
+#endif
 // RTMI_CHECK builds (analysis only) bounds-check every accumulator write and
 // count violations in segments[5..7] instead of performing them.
 #ifndef RTMI_CHECK
@@ -258,6 +261,9 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   if (lane == 0) wave_segs[wave] = 0;
   unsigned nseg = 0;  // world.hit calls of this lane (algorithmic-work accounting)
   RTMI_TRACE_BEGIN
+#if RTMI_TRACE_PHASES
+  PhaseClock phase_clock{{0, 0, 0}};
+#endif
 #if RTMI_STATS
   unsigned stats[4] = {0, 0, 0, 0};  // groups, groups with a candidate (wave), resolves (lane), sphere resolves (wave)
   unsigned bvh_stats[5] = {0, 0, 0, 0, 0};  // BVH: node visits, leaf sphere tests (lane); node iterations, leaf-sphere iterations, root resolutions (wave)
@@ -330,6 +336,9 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
 #if RTMI_STATS
                                        , bvh_stats
 #endif
+#if RTMI_TRACE_PHASES
+                                       , phase_clock
+#endif
         );
       } else {
         k = hit_world_packed<kPairGroup>(pairs, a.npairs, o, d, t
@@ -390,6 +399,11 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
         atomicAdd(&acc[wave][2][px], (unsigned long long)to_fixed(col.z));
         const int rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
         const int q = next + rank;
+#if RTMI_REGEN_TWICE
+        // analysis only: the regeneration executed twice (same result) to
+        // measure its marginal cost
+        if (q < nq) { int q2 = q; asm volatile("" : "+v"(q2)); start(q2); asm volatile("" : "+v"(px)); }
+#endif
         if (q < nq) start(q);
         else active = false;
       }
@@ -416,6 +430,9 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   atomicAdd(&segments[1], (unsigned long long)bvh_stats[2]);
   atomicAdd(&segments[2], (unsigned long long)bvh_stats[3]);
   atomicAdd(&segments[4], (unsigned long long)bvh_stats[4]);
+#endif
+#if RTMI_TRACE_PHASES
+  if (lane == 0) for (int q = 0; q < 3; ++q) atomicAdd(&segments[1 + q], phase_clock.c[q]);
 #endif
   RTMI_TRACE_END(1)
   if constexpr (CHUNKED) {
@@ -513,6 +530,9 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
   unsigned nseg = 0;
   int n_taken = 0;
   RTMI_TRACE_BEGIN
+#if RTMI_TRACE_PHASES
+  PhaseClock phase_clock{{0, 0, 0}};
+#endif
 #if RTMI_STATS
   unsigned stats[4] = {0, 0, 0, 0};
   unsigned bvh_stats[5] = {0, 0, 0, 0, 0};
@@ -663,6 +683,9 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
 #if RTMI_STATS
                                        , bvh_stats
 #endif
+#if RTMI_TRACE_PHASES
+                                       , phase_clock
+#endif
         );
       } else {
         k = hit_world_packed<kPairGroup>(pairs, a.npairs, o, d, t
@@ -775,7 +798,12 @@ __global__ __launch_bounds__(256) void debug_hit_kernel(const SpherePair *__rest
   out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1, bst) : hit_world_grid<kBigGroup>(acc, o, d, t1, bst);
 #else
   out_idx[2 * i] = hit_world_packed<kPairGroup>(pairs, npairs, o, d, t0);
+#if RTMI_TRACE_PHASES
+  PhaseClock pc{{0, 0, 0}};
+  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup>(acc, o, d, t1, pc);
+#else
   out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup>(acc, o, d, t1);
+#endif
 #endif
   out_t[2 * i] = t0;
   out_t[2 * i + 1] = t1;

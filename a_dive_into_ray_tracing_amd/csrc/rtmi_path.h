@@ -672,8 +672,13 @@ __device__ __forceinline__ void stage_bvh(const Accel &g) {
 // Grid LDS layout: nsph sphere float4s, then ncells + 1 uint16 cell starts,
 // nrefs uint16 refs, nsph uint16 scene indices (scenes of < 65536 spheres,
 // < 65536 refs).
+#ifndef RTMI_BIG_LDS
+#define RTMI_BIG_LDS 0
+#endif
+constexpr int kBigLdsPairs = 4;  // big-sphere pairs staged after the grid (RTMI_BIG_LDS)
 __host__ __device__ constexpr size_t grid_lds_bytes(int32_t nsph, int32_t ncells, int32_t nrefs) {
-  return (size_t(nsph) * 16 + (size_t(ncells) + 1) * 2 + size_t(nrefs) * 2 + size_t(nsph) * 2 + 15) / 16 * 16;
+  return (size_t(nsph) * 16 + (size_t(ncells) + 1) * 2 + size_t(nrefs) * 2 + size_t(nsph) * 2 + 15) / 16 * 16 +
+         (RTMI_BIG_LDS ? kBigLdsPairs * 32 : 0);
 }
 
 __device__ __forceinline__ void stage_grid(const Accel &g) {
@@ -683,6 +688,15 @@ __device__ __forceinline__ void stage_grid(const Accel &g) {
   for (int i = threadIdx.x; i < nstart; i += blockDim.x) u[i] = g.grid.cell_start[i];
   for (int i = threadIdx.x; i < g.grid.nrefs; i += blockDim.x) u[nstart + i] = g.grid.refs[i];
   for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) u[nstart + g.grid.nrefs + i] = uint16_t(g.sph_idx[i]);
+#if RTMI_BIG_LDS
+  {
+    const size_t off = (size_t(g.nsph) * 16 + (size_t(g.grid.ncells) + 1) * 2 + size_t(g.grid.nrefs) * 2 +
+                        size_t(g.nsph) * 2 + 15) / 16;
+    const float4 *src = reinterpret_cast<const float4 *>(g.big);
+    const int n4 = 2 * (g.nbig_pairs < kBigLdsPairs ? g.nbig_pairs : kBigLdsPairs);
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) rtmi_bvh_lds[off + i] = src[i];
+  }
+#endif
   __syncthreads();
 }
 
@@ -714,12 +728,27 @@ __device__ __forceinline__ float safe_inv(float v) {
 // computed directly from the cell index, never accumulated), so the cell the
 // DDA holds for any accepted hit point lists that sphere; a sphere tested in
 // several cells gives the same root each time.
+#ifndef RTMI_TRACE_PHASES
+#define RTMI_TRACE_PHASES 0
+#endif
+#if RTMI_TRACE_PHASES
+// analysis only: wave-level cycles (s_memtime) of the grid walk's phases:
+// [0] big spheres, [1] clip + DDA setup, [2] cell walk
+struct PhaseClock { unsigned long long c[3]; };
+#endif
+
 template <int GP>
 __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> o, V3<float> d, float &t_hit
 #if RTMI_STATS
                                                   , unsigned *gstats
 #endif
+#if RTMI_TRACE_PHASES
+                                                  , PhaseClock &pc
+#endif
                                                   ) {
+#if RTMI_TRACE_PHASES
+  const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
+#endif
   // ray terms of the expanded sphere test (as hit_world_bvh)
   const float a = dot<true>(d, d);
   const float inv_a = 1.0f / a;
@@ -749,10 +778,25 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
     const f2v DX = {d.x, d.x}, DY = {d.y, d.y}, DZ = {d.z, d.z}, KK = {K, K};
     const f2v MX = {mx, mx}, MY = {my, my}, MZ = {mz, mz};
     const f2v AA = {a, a}, AL = {aL, aL};
+#if RTMI_BIG_LDS
+    const SpherePair *big_lds = reinterpret_cast<const SpherePair *>(
+        rtmi_bvh_lds + (size_t(acc_s.nsph) * 16 + (size_t(acc_s.grid.ncells) + 1) * 2 + size_t(acc_s.grid.nrefs) * 2 +
+                        size_t(acc_s.nsph) * 2 + 15) / 16);
+#endif
     for (int32_t q = 0; q < acc_s.nbig_pairs; q += GP) {
       SpherePair p[GP];
+#if RTMI_BIG_LDS
+      if (acc_s.nbig_pairs <= kBigLdsPairs) {
+#pragma unroll
+        for (int g = 0; g < GP; ++g) p[g] = big_lds[q + g];
+      } else {
+#pragma unroll
+        for (int g = 0; g < GP; ++g) p[g] = acc_s.big[q + g];
+      }
+#else
 #pragma unroll
       for (int g = 0; g < GP; ++g) p[g] = acc_s.big[q + g];
+#endif
       f2v hb[GP], disc[GP];
       int ci[2 * GP];
       int any = 0;
@@ -777,6 +821,11 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
     }
   }
   // 2. the grid (staged in LDS by stage_grid)
+#if RTMI_TRACE_PHASES
+  const unsigned long long tp1 = __builtin_amdgcn_s_memtime();
+  pc.c[0] += tp1 - tp0;
+  unsigned long long tp2 = tp1;
+#endif
   const GridDesc &G = acc_s.grid;
   const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
   const float ox = -o.x * ix, oy = -o.y * iy, oz = -o.z * iz;
@@ -809,6 +858,9 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
     float tnx = tface(cx, sx, 0, ix, ox), tny = tface(cy, sy, 1, iy, oy), tnz = tface(cz, sz, 2, iz, oz);
     int cell = cx + G.n[0] * (cy + G.n[1] * cz);
     const int dcx = sx, dcy = sy * G.n[0], dcz = sz * G.n[0] * G.n[1];
+#if RTMI_TRACE_PHASES
+    tp2 = __builtin_amdgcn_s_memtime();
+#endif
     for (;;) {
 #if RTMI_STATS
       gstats[0] += 1;
@@ -872,6 +924,13 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
       }
     }
   }
+#if RTMI_TRACE_PHASES
+  {
+    const unsigned long long tp3 = __builtin_amdgcn_s_memtime();
+    pc.c[1] += tp2 - tp1;
+    pc.c[2] += tp3 - tp2;
+  }
+#endif
   t_hit = t_max;
   return best;
 }

@@ -53,6 +53,8 @@ hw = (raw[:, 2] >> np.uint64(32)).astype(np.int64)
 print(f"{kind} strip_of={strip_of} chunk={chunk} tail={tail}/{tchunk}: waves {n}, span {span / 1e3:.2f} ms, "
       f"items {items.sum()}, segs/wave-line mean {segs.mean():.0f}")
 print(f"cycles in hit_world_packed / wave lifetime: {cnt[5] / max(cnt[6], 1):.3f}")
+if os.environ.get("TRACE_PHASES"):
+    print(f"grid phases / wave lifetime: big spheres {cnt[1] / max(cnt[6], 1):.3f}, clip+setup {cnt[2] / max(cnt[6], 1):.3f}, cell walk {cnt[3] / max(cnt[6], 1):.3f}")
 print("wave end percentiles (ms):", " ".join(f"p{q}={np.percentile(t1, q) / 1e3:.2f}" for q in (1, 10, 50, 90, 99, 100)))
 print("wave duration percentiles (ms):", " ".join(f"p{q}={np.percentile(t1 - t0, q) / 1e3:.3f}" for q in (1, 10, 50, 90, 99, 100)))
 bins = np.linspace(0, span, 21)

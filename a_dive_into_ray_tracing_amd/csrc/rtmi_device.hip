@@ -69,6 +69,11 @@ struct RenderArgs {
   // together instead of each wave ramping down alone (same image: the
   // accumulators are fixed point, their sums independent of who adds)
   int32_t block_pool;
+  // block_flush launches whose block covers ALL samples of its tile (items
+  // per tile == waves per block, not a progressive pass): the block writes the
+  // tile's float sums straight to the output strip — no accumulator memset,
+  // global atomics or finalize pass (config 2: 500 spp = 4 items of 125)
+  int32_t block_owns_tile;
   // progressive passes: this launch renders samples s_base + [0, spp)
   int32_t s_base;
   uint64_t out_elems;  // elements of accum / out (RTMI_CHECK builds verify every write)
@@ -445,7 +450,8 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
           unsigned long long v = 0;
 #pragma unroll
           for (int w = 0; w < WPB; ++w) v += acc[w][c][lane];
-          atomicAdd(&accum[o3 + c], v);
+          if (a.block_owns_tile) out[o3 + c] = from_fixed((long long)v);
+          else atomicAdd(&accum[o3 + c], v);
         }
       }
       return;
@@ -939,6 +945,9 @@ struct rt_ctx {
   // block-shared job pool of block_flush launches (same image; measured
   // neutral, DESIGN.md §5, so off unless RTMI_BLOCK_POOL=1)
   bool block_pool = std::getenv("RTMI_BLOCK_POOL") && std::getenv("RTMI_BLOCK_POOL")[0] == '1';
+  // a block that covers all samples of its tile writes the floats itself
+  // (RTMI_BLOCK_OWNS=0 routes it through the accumulator, for A/B and tests)
+  bool block_owns = !(std::getenv("RTMI_BLOCK_OWNS") && std::getenv("RTMI_BLOCK_OWNS")[0] == '0');
   // the schedule of the last launch (rt_ctx_last_schedule, for tests)
   int32_t last_sched[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned *cost_prev = nullptr, *cost_cur = nullptr, *cost_sorted = nullptr;
@@ -1646,15 +1655,17 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   a.tiles = int32_t(tiles); a.spp1 = spp1; a.chunk1 = chunk1; a.nch1 = nch1; a.chunk2 = chunk2; a.nch2 = nch2;
   a.block_flush = !persistent && nch2 == 0 && nch1 % grid_wpb == 0 && ctx->block_flush;
   a.block_pool = a.block_flush && ctx->block_pool;
+  a.block_owns_tile = a.block_flush && !pass_accum && nch1 == grid_wpb && ctx->block_owns;
   if (!ctx->probing) {
-    const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush, a.block_pool, persistent ? 1 : 0, acc_kind};
+    const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush + a.block_owns_tile, a.block_pool, persistent ? 1 : 0,
+                              acc_kind};
     std::copy(sched, sched + 8, ctx->last_sched);
   }
   a.s_base = s_base;
   a.out_elems = uint64_t(nvalid) * uint64_t(W) * 3;
   const bool chunked = pass_accum || nch1 + nch2 > 1;
   const size_t n_valid_out = size_t(nvalid) * W * 3;
-  if (chunked && !pass_accum) {
+  if (chunked && !pass_accum && !a.block_owns_tile) {
     if (ctx->accum_cap < n_valid_out) {
       int rc = dev_alloc(&ctx->accum, n_valid_out);
       if (rc) { ctx->accum_cap = 0; return rc; }
@@ -1666,9 +1677,9 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   unsigned long long *const accum = pass_accum ? pass_accum : ctx->accum;
   // host-side check of what the kernels will index: accumulator and output
   // hold the nvalid rows, every work item lies inside them
-  if (chunked && (!accum || (pass_accum ? ctx->pass_cap : ctx->accum_cap) < n_valid_out))
+  if (chunked && !a.block_owns_tile && (!accum || (pass_accum ? ctx->pass_cap : ctx->accum_cap) < n_valid_out))
     return set_error(RT_EHIP, "internal: accumulator not allocated for %zu elements", n_valid_out);
-  if (!chunked && !strip) return set_error(RT_EHIP, "internal: no output strip");
+  if ((!chunked || a.block_owns_tile) && !strip) return set_error(RT_EHIP, "internal: no output strip");
   if (int64_t(tiles_y) * TH < nvalid || int64_t(tiles_x) * TW < W || nch1 * int64_t(chunk1) < spp1 ||
       nch2 * int64_t(chunk2) < spp - spp1)
     return set_error(RT_EHIP, "internal: work items do not cover the image");
@@ -1747,7 +1758,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     default: launch_shape<64>(persistent, acc_kind, chunked, grid, st, ctx, a, accum, strip); break;
   }
   HIP_TRY(hipGetLastError());
-  if (chunked && !pass_accum) {
+  if (chunked && !pass_accum && !a.block_owns_tile) {
     hipLaunchKernelGGL(finalize_kernel, dim3(unsigned((n_valid_out + 255) / 256)), dim3(256), 0, st, ctx->accum,
                        strip, n_valid_out);
     HIP_TRY(hipGetLastError());

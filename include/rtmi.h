@@ -188,7 +188,8 @@ int rt_render_rows(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int3
 int rt_ctx_last_segments(rt_ctx *ctx, uint64_t *segments);
 /* Diagnostic: the schedule of the context's last launch (not its probe):
  * {tile width, samples per item, items per tile, tail items per tile,
- *  block flush, block pool, persistent kernel, BVH}. */
+ *  block flush (2: the block owns its tile and writes the floats), block
+ *  pool, persistent kernel, accelerator (0 none, 1 BVH, 2 grid)}. */
 int rt_ctx_last_schedule(rt_ctx *ctx, int32_t *out8);
 /* Block until the context's stream is idle. */
 int rt_ctx_synchronize(rt_ctx *ctx);

@@ -451,18 +451,21 @@ def test_cost_ordered_dispatch_same_image(kernel, accel, final_world, final_rend
 @pytest.mark.parametrize("W,H,S", [(40, 24, 37), (29, 19, 37), (29, 19, 5)])
 def test_block_flush_same_image(accel, W, H, S, final_world, monkeypatch):
     """The automatic grid schedule gives every block exactly 4 items of one
-    tile and flushes the block's summed accumulators once.  RTMI_BLOCK_POOL=1
-    makes the block's waves draw (pixel, sample) jobs from one block-wide
-    pool; RTMI_BLOCK_FLUSH=0 flushes per wave.  Same image and world.hit count
+    tile and flushes the block's summed accumulators once — here the block
+    owns its tile and writes the floats itself (RTMI_BLOCK_OWNS=0: through
+    the accumulator).  RTMI_BLOCK_POOL=1 makes the block's waves draw
+    (pixel, sample) jobs from one block-wide pool; RTMI_BLOCK_FLUSH=0 flushes
+    per wave.  Same image and world.hit count
     bit for bit, equal to the oracle.  37 spp: items of 10/10/10/7 samples;
     29x19: partial tiles (automatic 16x4 shape); 29x19 at 5 spp: items of
     2/2/1/0 samples (the empty item's wave only joins the flush).  The launch
     schedule is read back, so the test cannot pass on a path it skipped."""
     cam = rt.final_camera(W / H)
     imgs, segs = [], []
-    for flush, pool in (("1", "1"), ("1", "0"), ("0", "1")):
+    for flush, pool, owns in (("1", "1", "1"), ("1", "0", "1"), ("0", "1", "1"), ("1", "0", "0")):
         monkeypatch.setenv("RTMI_BLOCK_FLUSH", flush)
         monkeypatch.setenv("RTMI_BLOCK_POOL", pool)
+        monkeypatch.setenv("RTMI_BLOCK_OWNS", owns)
         r = rt.Renderer(final_world, 0)
         try:
             r.set_kernel("grid")
@@ -473,11 +476,13 @@ def test_block_flush_same_image(accel, W, H, S, final_world, monkeypatch):
         finally:
             r.close()
         assert sch["items_per_tile"] == 4 and sch["persistent"] == 0, sch
-        assert sch["block_flush"] == int(flush == "1") and sch["block_pool"] == int(flush == "1" and pool == "1"), sch
+        # 4 items per tile on 4-wave blocks: the block owns its tile (2)
+        assert sch["block_flush"] == (0 if flush == "0" else (2 if owns == "1" else 1)), sch
+        assert sch["block_pool"] == int(flush == "1" and pool == "1"), sch
         if S == 5:
             assert sch["chunk"] == 2  # 2, 2, 1, 0 samples
-    assert np.array_equal(imgs[0], imgs[1]) and np.array_equal(imgs[0], imgs[2])
-    assert segs[0] == segs[1] == segs[2]
+    assert all(np.array_equal(imgs[0], im) for im in imgs[1:])
+    assert all(sg == segs[0] for sg in segs)
     want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
     assert np.array_equal(imgs[0], want)
 

@@ -189,6 +189,51 @@ template <bool BVH> struct GridShape {
   static constexpr int waves = BVH ? RTMI_BVH_WAVES : kWavesPerBlock;
   static constexpr int per_eu = BVH ? RTMI_ACC_PER_EU : RTMI_WAVES_PER_EU;
 };
+// Persistent-kernel block shape.  The accelerated kernels run 8-wave blocks at
+// 8 waves per SIMD (64 VGPRs): a resident grid holds its slots to the end, so
+// big blocks cost no fragmentation, and 8 waves share one staged copy of the
+// BVH/grid beside their two accumulator slots each (~35 KB: 4 blocks per CU).
+#ifndef RTMI_PERSIST_ACC_WAVES
+#define RTMI_PERSIST_ACC_WAVES 8
+#endif
+template <int ACC> struct PersistShape {
+  static constexpr int waves = ACC ? RTMI_PERSIST_ACC_WAVES : kWavesPerBlock;
+  static constexpr int per_eu = ACC ? RTMI_ACC_PER_EU : RTMI_PERSIST_MIN_BLOCKS;
+};
+
+#if RTMI_CAM_LDS
+// The camera and the (W-1, H-1) denominators of main.cpp:278-279 in LDS
+// (21 floats), read at each regeneration instead of held in scalar registers.
+__device__ __forceinline__ void stage_camera(float *cam_lds, const RenderArgs &a) {
+  const unsigned t = threadIdx.x;
+  if (t < 19) {
+    float v;
+    switch (t / 3) {
+      case 0: v = (&a.cam.origin.x)[t % 3]; break;
+      case 1: v = (&a.cam.llc.x)[t % 3]; break;
+      case 2: v = (&a.cam.hor.x)[t % 3]; break;
+      case 3: v = (&a.cam.ver.x)[t % 3]; break;
+      case 4: v = (&a.cam.u.x)[t % 3]; break;
+      case 5: v = (&a.cam.v.x)[t % 3]; break;
+      default: v = a.cam.lens; break;
+    }
+    cam_lds[t] = v;
+  } else if (t < 21) {
+    cam_lds[t] = float((t == 19 ? a.W : a.H) - 1);
+  }
+}
+__device__ __forceinline__ Cam<float> lds_camera(const float *cam_lds) {
+  Cam<float> cm;
+  cm.origin = mk(cam_lds[0], cam_lds[1], cam_lds[2]);
+  cm.llc = mk(cam_lds[3], cam_lds[4], cam_lds[5]);
+  cm.hor = mk(cam_lds[6], cam_lds[7], cam_lds[8]);
+  cm.ver = mk(cam_lds[9], cam_lds[10], cam_lds[11]);
+  cm.u = mk(cam_lds[12], cam_lds[13], cam_lds[14]);
+  cm.v = mk(cam_lds[15], cam_lds[16], cam_lds[17]);
+  cm.lens = cam_lds[18];
+  return cm;
+}
+#endif
 // ACC: 0 brute force, 1 BVH, 2 uniform grid (RT_ACCEL_*); the accelerated
 // kernels stage their structure in LDS and share the block shape.
 template <int TW, bool CHUNKED, int ACC>
@@ -268,6 +313,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   RTMI_TRACE_BEGIN
 #if RTMI_TRACE_PHASES
   PhaseClock phase_clock{{0, 0, 0}};
+  unsigned long long cyc_iter = 0, cyc_regen = 0, cyc_ramp = 0;
 #endif
 #if RTMI_STATS
   unsigned stats[4] = {0, 0, 0, 0};  // groups, groups with a candidate (wave), resolves (lane), sphere resolves (wave)
@@ -323,6 +369,9 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
     if (__ballot(active) == 0) break;
     bool done = false;
     V3<float> col = mk(0.f, 0.f, 0.f);
+#if RTMI_TRACE_PHASES
+    const unsigned long long cyc_a = __builtin_amdgcn_s_memtime();
+#endif
     if (active) {
       float t;
       ++nseg;
@@ -391,6 +440,11 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
         }
       }
     }
+#if RTMI_TRACE_PHASES
+    const unsigned long long cyc_b = __builtin_amdgcn_s_memtime();
+    cyc_iter += cyc_b - cyc_a;  // hit + shading of this pass (wave-level)
+    const bool ramp = next >= nq;  // the item's jobs all taken: the wave's ramp-down
+#endif
     const unsigned long long m = __ballot(done);
     if (m) {
       if (pool) {  // claim popcount(m) jobs of the block pool (one LDS atomic)
@@ -414,6 +468,11 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
       }
       next += __popcll(m);
     }
+#if RTMI_TRACE_PHASES
+    const unsigned long long cyc_e = __builtin_amdgcn_s_memtime();
+    cyc_regen += cyc_e - cyc_b;
+    if (ramp) cyc_ramp += cyc_e - cyc_a;
+#endif
   }
 
   atomicAdd(&wave_segs[wave], (unsigned long long)nseg);
@@ -437,7 +496,13 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   atomicAdd(&segments[4], (unsigned long long)bvh_stats[4]);
 #endif
 #if RTMI_TRACE_PHASES
+  // [1] big spheres + clip/setup, [2] loop passes after the item's last job
+  // was taken (ramp-down), [3] cell walk
+  phase_clock.c[0] += phase_clock.c[1];
+  phase_clock.c[1] = cyc_ramp;
   if (lane == 0) for (int q = 0; q < 3; ++q) atomicAdd(&segments[1 + q], phase_clock.c[q]);
+  // wave-level: [4] hit + shading passes, [7] accumulation + regeneration
+  if (lane == 0) { atomicAdd(&segments[4], cyc_iter); atomicAdd(&segments[7], cyc_regen); }
 #endif
   RTMI_TRACE_END(1)
   if constexpr (CHUNKED) {
@@ -518,15 +583,25 @@ __device__ __forceinline__ ItemDesc describe_item(const RenderArgs &a, int item)
 }
 
 template <int TW, bool CHUNKED, int ACC>
-__global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void render_persistent(
+__global__ __launch_bounds__(64 * PersistShape<ACC>::waves, PersistShape<ACC>::per_eu) void render_persistent(
     const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1,
     const SpherePair *__restrict__ pairs, RenderArgs a, unsigned long long *__restrict__ accum,
     float *__restrict__ out, unsigned long long *__restrict__ segments, unsigned *__restrict__ counter) {
-  __shared__ unsigned long long acc[kWavesPerBlock][2][3][64];
-  __shared__ unsigned long long wave_segs[kWavesPerBlock];
-  __shared__ unsigned slot_segs[kWavesPerBlock][2];  // world.hit calls of each slot's item (tile cost)
+  constexpr int WPB = PersistShape<ACC>::waves;
+  __shared__ unsigned long long acc[WPB][2][3][64];
+  __shared__ unsigned long long wave_segs[WPB];
+  __shared__ unsigned slot_segs[WPB][2];  // world.hit calls of each slot's item (tile cost)
+  // each slot's item: x0, y0, vw, nv, s_base + s0, tile, 1/nv, 1/vw (float
+  // bits), read at regeneration and flush: the wave's registers hold only
+  // the current item's job counters
+  __shared__ int item_lds[WPB][2][8];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
+#if RTMI_CAM_LDS
+  __shared__ float cam_lds[21];
+  stage_camera(cam_lds, a);
+  if constexpr (ACC == 0) __syncthreads();  // (accelerated kernels: stage_* ends with one)
+#endif
   if constexpr (ACC == 1) stage_bvh(a.acc);
   else if constexpr (ACC == 2) stage_grid(a.acc);
   if (lane < 2) slot_segs[wave][lane] = 0;
@@ -558,23 +633,23 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
 #endif
   // wave-uniform slot state: the current item (slot `cur`) hands out jobs;
   // the previous one (slot cur^1, all jobs handed out) may still have paths
-  // in flight.  Fixed-name variables, no arrays: they stay in SGPRs.
+  // in flight.
   int cur = 0;
   bool cur_valid = false, prev_valid = false, exhausted = false;
-  int cur_next = 0;
-  ItemDesc cd{0, 0, 1, 0, 0, 0, 0}, pd{0, 0, 1, 0, 0, 0, 0};
+  int cur_next = 0, cur_nq = 0;
 
-  // per-lane path state
+  // per-lane path state; px = pixel of the tile | slot << 6
   V3<float> o, d, T;
-  int px = 0, depth = 0, lane_slot = 0, path_segs = 0;
+  int px = 0, depth = 0;
   bool active = false;
   Xoro rng;
 
-  auto flush = [&](int s, const ItemDesc &it) {
+  auto flush = [&](int s) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (lane < it.nv) {
-      const int ly = lane / it.vw, lx = lane - ly * it.vw;
-      const size_t o3 = (size_t(it.y0 + ly) * size_t(a.W) + size_t(it.x0 + lx)) * 3;
+    const int x0 = item_lds[wave][s][0], y0 = item_lds[wave][s][1], vw = item_lds[wave][s][2];
+    if (lane < item_lds[wave][s][3]) {
+      const int ly = lane / vw, lx = lane - ly * vw;
+      const size_t o3 = (size_t(y0 + ly) * size_t(a.W) + size_t(x0 + lx)) * 3;
 #if RTMI_CHECK
       if (o3 + 3 > a.out_elems || s < 0 || s > 1) {
         atomicAdd(&segments[5], 1ull);
@@ -589,7 +664,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
     }
     for (int c = 0; c < 3; ++c) acc[wave][s][c][lane] = 0;
     if (lane == 0) {
-      if (a.tile_cost) atomicAdd(&a.tile_cost[it.tile], slot_segs[wave][s]);
+      if (a.tile_cost) atomicAdd(&a.tile_cost[item_lds[wave][s][5]], slot_segs[wave][s]);
       slot_segs[wave][s] = 0;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -599,26 +674,36 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
     // 1. hand jobs to idle lanes, fetching items as the current one runs dry
     unsigned long long idle = __ballot(!active);
     while (idle) {
-      if (cur_valid && cur_next < cd.nq) {
-        const int avail = cd.nq - cur_next;
+      if (cur_valid && cur_next < cur_nq) {
+        const int avail = cur_nq - cur_next;
         const int rank = __builtin_amdgcn_mbcnt_hi(unsigned(idle >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(idle), 0u));
         if (((idle >> lane) & 1ull) && rank < avail) {
           // job q -> pixel q % nv, sample s0 + q / nv; then the camera ray
+          // (q < nq <= 64 * 65535 < 2^22: div_small is exact, host-checked)
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // item and camera read here
+          const int *it = item_lds[wave][cur];
+          const int nv = it[3], vw = it[2];
           const int q = cur_next + rank;
-          const int qs = q / cd.nv;
-          px = q - qs * cd.nv;
-          const int ly = px / cd.vw, lx = px - ly * cd.vw;
-          const int i = cd.x0 + lx;
-          const int j = a.row0 + (cd.y0 + ly) * a.row_step;
-          rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(a.s_base + cd.s0 + qs));
+          const int qs = div_small(q, nv, __int_as_float(it[6]));
+          const int p = q - qs * nv;
+          const int ly = div_small(p, vw, __int_as_float(it[7])), lx = p - ly * vw;
+          const int i = it[0] + lx;
+          const int j = a.row0 + (it[1] + ly) * a.row_step;
+          rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(it[4] + qs));
           float ju, jv;
           rng.pair(ju, jv);
+#if RTMI_CAM_LDS
+          const float u = (float(i) + ju) / cam_lds[19];  // main.cpp:278
+          const float v = (float(j) + jv) / cam_lds[20];  // main.cpp:279
+          get_ray<true, float>(lds_camera(cam_lds), u, v, rng, o, d);
+#else
           const float u = (float(i) + ju) / float(a.W - 1);  // main.cpp:278
           const float v = (float(j) + jv) / float(a.H - 1);  // main.cpp:279
           get_ray<true, float>(a.cam, u, v, rng, o, d);
+#endif
           T = mk(1.f, 1.f, 1.f);
           depth = 0;
-          lane_slot = cur;
+          px = p | (cur << 6);
           active = true;
         }
         cur_next += min(__popcll(idle), avail);
@@ -637,19 +722,35 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
         // some waves starve (10x spread of work per wave) and end up holding
         // the last items alone.  A wave behind the average item count raises
         // its issue priority until it has caught up.
-        if (n_taken * int(gridDim.x) * kWavesPerBlock < int(itn)) __builtin_amdgcn_s_setprio(2);
+        if (n_taken * int(gridDim.x) * WPB < int(itn)) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(0);
 #endif
         ++n_taken;
         prev_valid = cur_valid;  // all its jobs are handed out
-        pd = cd;
         cur ^= 1;
-        cd = describe_item<TW>(a, int(itn));
+        const ItemDesc cd = describe_item<TW>(a, int(itn));
+        if (lane < 8) {
+          const int f[8] = {cd.x0, cd.y0, cd.vw, cd.nv, a.s_base + cd.s0, cd.tile,
+                            __float_as_int(1.0f / float(max(cd.nv, 1))), __float_as_int(1.0f / float(cd.vw))};
+          int v = f[0];
+#pragma unroll
+          for (int k = 1; k < 8; ++k) v = lane == k ? f[k] : v;
+          item_lds[wave][cur][lane] = v;
+        }
+        cur_nq = cd.nq;
         cur_valid = true;
         cur_next = 0;
       }
     }
-    if (__ballot(active) == 0) break;
+    const unsigned long long live = __ballot(active);
+    if (live == 0) break;
+    {  // world.hit calls per slot (the tiles' cost map)
+      const unsigned long long live_cur = __ballot(active && (px >> 6) == cur);
+      if (lane == 0) {
+        if (live_cur) atomicAdd(&slot_segs[wave][cur], unsigned(__popcll(live_cur)));
+        if (live != live_cur) atomicAdd(&slot_segs[wave][cur ^ 1], unsigned(__popcll(live & ~live_cur)));
+      }
+    }
 #if RTMI_FAIR == 3
     // The SIMD issues the oldest ready wave first: in a resident grid the
     // youngest wave of a SIMD gets ~1/10 of the oldest one's issue slots and
@@ -673,7 +774,6 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
     if (active) {
       float t;
       ++nseg;
-      ++path_segs;
 #if RTMI_TRACE
       const unsigned long long cyc0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -737,32 +837,31 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
     }
     // 3. finished paths add their colour to their item's slot
 #if RTMI_CHECK
-    if (done && (px < 0 || px > 63 || lane_slot < 0 || lane_slot > 1)) {
+    if (done && (px < 0 || px > 127)) {
       atomicAdd(&segments[7], 1ull);
       done = false;
       active = false;
     }
 #endif
     if (done) {
-      atomicAdd(&slot_segs[wave][lane_slot], unsigned(path_segs));
-      path_segs = 0;
-      atomicAdd(&acc[wave][lane_slot][0][px], (unsigned long long)to_fixed(col.x));
-      atomicAdd(&acc[wave][lane_slot][1][px], (unsigned long long)to_fixed(col.y));
-      atomicAdd(&acc[wave][lane_slot][2][px], (unsigned long long)to_fixed(col.z));
+      const int s = px >> 6, p = px & 63;
+      atomicAdd(&acc[wave][s][0][p], (unsigned long long)to_fixed(col.x));
+      atomicAdd(&acc[wave][s][1][p], (unsigned long long)to_fixed(col.y));
+      atomicAdd(&acc[wave][s][2][p], (unsigned long long)to_fixed(col.z));
       active = false;
     }
     // 4. flush items whose jobs are all handed out and whose paths are all done
-    if (prev_valid && __ballot(active && lane_slot != cur) == 0) {
-      flush(cur ^ 1, pd);
+    if (prev_valid && __ballot(active && (px >> 6) != cur) == 0) {
+      flush(cur ^ 1);
       prev_valid = false;
     }
-    if (cur_valid && cur_next >= cd.nq && __ballot(active && lane_slot == cur) == 0) {
-      flush(cur, cd);
+    if (cur_valid && cur_next >= cur_nq && __ballot(active && (px >> 6) == cur) == 0) {
+      flush(cur);
       cur_valid = false;
     }
   }
-  if (prev_valid) flush(cur ^ 1, pd);
-  if (cur_valid) flush(cur, cd);
+  if (prev_valid) flush(cur ^ 1);
+  if (cur_valid) flush(cur);
 
   atomicAdd(&wave_segs[wave], (unsigned long long)nseg);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1411,8 +1510,8 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
     ctx->nnodes = lds <= kBvhLdsMax && n <= 65535 ? int32_t(b.nodes.size()) : 0;
     int per_cu = 0;
     if (ctx->nnodes)
-      HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<8, true, true>,
-                                                           64 * kWavesPerBlock, lds));
+      HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<8, true, 1>,
+                                                           64 * PersistShape<1>::waves, lds));
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     ctx->resident_blocks_bvh = std::max(1, per_cu) * cus;
@@ -1438,7 +1537,7 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
       const size_t glds = grid_lds_bytes(ctx->ngrid_sph, ctx->grid.ncells, ctx->grid.nrefs);
       per_cu = 0;
       HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<8, true, 2>,
-                                                           64 * kWavesPerBlock, glds));
+                                                           64 * PersistShape<2>::waves, glds));
       ctx->resident_blocks_grid = std::max(1, per_cu) * cus;
     }
   }
@@ -1525,10 +1624,10 @@ void launch_persistent(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ct
                        unsigned long long *accum, float *out) {
   const size_t lds = accel_lds_bytes(a.acc, ACC);
   if (chunked)
-    hipLaunchKernelGGL((render_persistent<TW, true, ACC>), grid, dim3(64 * kWavesPerBlock), lds, st, ctx->geom, ctx->sh0,
+    hipLaunchKernelGGL((render_persistent<TW, true, ACC>), grid, dim3(64 * PersistShape<ACC>::waves), lds, st, ctx->geom, ctx->sh0,
                        ctx->sh1, ctx->pairs, a, accum, out, ctx->segments, ctx->counter);
   else
-    hipLaunchKernelGGL((render_persistent<TW, false, ACC>), grid, dim3(64 * kWavesPerBlock), lds, st, ctx->geom,
+    hipLaunchKernelGGL((render_persistent<TW, false, ACC>), grid, dim3(64 * PersistShape<ACC>::waves), lds, st, ctx->geom,
                        ctx->sh0, ctx->sh1, ctx->pairs, a, accum, out, ctx->segments, ctx->counter);
 }
 
@@ -1625,7 +1724,10 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   }
   if (chunk2 <= 0) chunk2 = std::max(1, chunk1 / 4);
   if (tail < 0) tail = 0;  // automatic: no short-item phase (it measured no better)
-  chunk1 = std::min(chunk1, spp);
+  // at most 65535 samples per item: job indices (< 64 * chunk) stay below
+  // 2^22, where the kernels' float-reciprocal division (div_small) is exact
+  chunk1 = std::min({chunk1, spp, 65535});
+  chunk2 = std::min(chunk2, 65535);
   tail = std::min(tail, spp);
   const int32_t spp1 = spp - tail;
   const int64_t grid_wpb = bvh ? GridShape<true>::waves : GridShape<false>::waves;
@@ -1743,10 +1845,12 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   if (persistent) {
     // a resident grid of waves pulling items from a global counter
     HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
+    const int64_t pw = acc_kind == 1 ? PersistShape<1>::waves : acc_kind == 2 ? PersistShape<2>::waves
+                                                                                : PersistShape<0>::waves;
     const int64_t waves =
         std::min<int64_t>(items, int64_t(acc_kind == 1 ? ctx->resident_blocks_bvh
-                                         : acc_kind == 2 ? ctx->resident_blocks_grid : ctx->resident_blocks) * kWavesPerBlock);
-    grid = dim3(unsigned((waves + kWavesPerBlock - 1) / kWavesPerBlock));
+                                         : acc_kind == 2 ? ctx->resident_blocks_grid : ctx->resident_blocks) * pw);
+    grid = dim3(unsigned((waves + pw - 1) / pw));
   } else {
     const int64_t wpb = bvh ? GridShape<true>::waves : GridShape<false>::waves;
     grid = dim3(unsigned((items + wpb - 1) / wpb));

@@ -54,7 +54,8 @@ print(f"{kind} strip_of={strip_of} chunk={chunk} tail={tail}/{tchunk}: waves {n}
       f"items {items.sum()}, segs/wave-line mean {segs.mean():.0f}")
 print(f"cycles in hit_world_packed / wave lifetime: {cnt[5] / max(cnt[6], 1):.3f}")
 if os.environ.get("TRACE_PHASES"):
-    print(f"grid phases / wave lifetime: big spheres {cnt[1] / max(cnt[6], 1):.3f}, clip+setup {cnt[2] / max(cnt[6], 1):.3f}, cell walk {cnt[3] / max(cnt[6], 1):.3f}")
+    print(f"grid phases / wave lifetime: big spheres + clip/setup {cnt[1] / max(cnt[6], 1):.3f}, ramp-down passes {cnt[2] / max(cnt[6], 1):.3f}, cell walk {cnt[3] / max(cnt[6], 1):.3f}")
+    print(f"loop passes / wave lifetime: hit + shading {cnt[4] / max(cnt[6], 1):.3f}, accumulation + regeneration {cnt[7] / max(cnt[6], 1):.3f}")
 print("wave end percentiles (ms):", " ".join(f"p{q}={np.percentile(t1, q) / 1e3:.2f}" for q in (1, 10, 50, 90, 99, 100)))
 print("wave duration percentiles (ms):", " ".join(f"p{q}={np.percentile(t1 - t0, q) / 1e3:.3f}" for q in (1, 10, 50, 90, 99, 100)))
 bins = np.linspace(0, span, 21)

@@ -166,7 +166,8 @@ __device__ __forceinline__ int div_small(int q, int d, float inv_d) {
 }
 
 __device__ __forceinline__ int64_t to_fixed(float c) {
-  const float g = c == c ? (c > 64.0f ? 64.0f : (c < -64.0f ? -64.0f : c)) : 0.0f;
+  // branch-free: v_med3 clamps (inf included), NaN selects 0
+  const float g = c == c ? __builtin_amdgcn_fmed3f(c, -64.0f, 64.0f) : 0.0f;
   return int64_t(g * 4294967296.0f);
 }
 __device__ __forceinline__ float from_fixed(int64_t v) { return float(v) * 0x1p-32f; }

@@ -64,7 +64,7 @@ constexpr size_t kPLdsBudget = 136 * 1024;                    // persistent kern
 
 // NaN -> 0, clamped to [-64, 64]: as rtmi_device.hip to_fixed (and the oracle)
 __device__ __forceinline__ int64_t fixed(float c) {
-  const float g = c == c ? (c > 64.0f ? 64.0f : (c < -64.0f ? -64.0f : c)) : 0.0f;
+  const float g = c == c ? __builtin_amdgcn_fmed3f(c, -64.0f, 64.0f) : 0.0f;  // branch-free guard
   return int64_t(g * 4294967296.0f);
 }
 

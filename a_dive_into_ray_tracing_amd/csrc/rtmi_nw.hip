@@ -62,15 +62,38 @@ constexpr size_t kLdsBudget = size_t(RTMI_NW_LDS_KB) * 1024;  // grid kernel: st
 constexpr int kPWaves = 16;                                   // persistent kernel: waves per block (one per CU)
 constexpr size_t kPLdsBudget = 136 * 1024;                    // persistent kernel: staged bytes (+ 24 KB accumulators)
 
+// RTMI_NW_PHASES builds (analysis only): wave-level cycles (s_memtime) of a
+// work item's loop passes: [0] closest hit, [1] hit record + texture +
+// scatter, [2] accumulation + regeneration, [3] whole item; read with
+// rt_nw_debug_phases.
+#ifndef RTMI_NW_PHASES
+#define RTMI_NW_PHASES 0
+#endif
+#if RTMI_NW_PHASES
+__device__ unsigned long long g_nw_phase[4];
+#endif
+
 // NaN -> 0, clamped to [-64, 64]: as rtmi_device.hip to_fixed (and the oracle)
 __device__ __forceinline__ int64_t fixed(float c) {
   const float g = c == c ? __builtin_amdgcn_fmed3f(c, -64.0f, 64.0f) : 0.0f;  // branch-free guard
   return int64_t(g * 4294967296.0f);
 }
 
-template <bool LDS_NODES, bool LDS_OBJS>
+template <bool LDS_NODES, bool LDS_OBJS, bool GRID>
 __device__ __forceinline__ void stage_scene(const View &sc) {
-  if constexpr (LDS_NODES) {  // BVH nodes (lo[], hi[]), then objects and their insertion indices
+  if constexpr (GRID) {  // objects, insertion indices, cell starts, refs, brute-force list (nw_grid_lds_bytes)
+    const float4 *src = reinterpret_cast<const float4 *>(sc.obj);
+    for (int i = threadIdx.x; i < 3 * sc.nobj; i += blockDim.x) nw_nodes_lds[i] = src[i];
+    int32_t *ids = reinterpret_cast<int32_t *>(nw_nodes_lds + 3 * sc.nobj);
+    for (int i = threadIdx.x; i < sc.nobj; i += blockDim.x) ids[i] = sc.obj_id[i];
+    uint16_t *u = reinterpret_cast<uint16_t *>(ids + sc.nobj);
+    const int nstart = sc.grid.ncells + 1;
+    for (int i = threadIdx.x; i < nstart; i += blockDim.x) u[i] = sc.grid.cell_start[i];
+    for (int i = threadIdx.x; i < sc.grid.nrefs; i += blockDim.x) u[nstart + i] = sc.grid.refs[i];
+    int32_t *big = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(u) + ((size_t(nstart) + sc.grid.nrefs) * 2 + 3) / 4 * 4);
+    for (int i = threadIdx.x; i < sc.nbig; i += blockDim.x) big[i] = sc.gbig[i];
+    __syncthreads();
+  } else if constexpr (LDS_NODES) {  // BVH nodes (lo[], hi[]), then objects and their insertion indices
     for (int i = threadIdx.x; i < sc.nnodes; i += blockDim.x) {
       nw_nodes_lds[i] = sc.nlo[i];
       nw_nodes_lds[sc.nnodes + i] = sc.nhi[i];
@@ -89,7 +112,7 @@ __device__ __forceinline__ void stage_scene(const View &sc) {
 // One work item = (8x8 tile, <= chunk samples) on one wave: lanes pull
 // (pixel, sample) jobs from the item's queue and regenerate paths as theirs
 // end; sums in the wave's LDS accumulator, then one global add per pixel.
-template <bool CHUNKED, bool LDS_NODES, bool LDS_OBJS>
+template <bool CHUNKED, bool LDS_NODES, bool LDS_OBJS, bool GRID>
 __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item, int lane,
                                          unsigned long long (&acc)[3][64], unsigned long long *__restrict__ accum,
                                          float *__restrict__ out, unsigned &nseg) {
@@ -128,6 +151,10 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
     depth = 0;
   };
 
+#if RTMI_NW_PHASES
+  unsigned long long ph[4] = {0, 0, 0, 0}, pa = 0, pb = 0;
+  const unsigned long long p_start = __builtin_amdgcn_s_memtime();
+#endif
   bool active = lane < nq;
   if (active) start(lane);
   int next = 64;
@@ -135,12 +162,19 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
     if (__ballot(active) == 0) break;
     bool done = false;
     V col = mk(0.f, 0.f, 0.f);
+#if RTMI_NW_PHASES
+    pa = __builtin_amdgcn_s_memtime();
+#endif
     if (active) {
       ++nseg;
       const uint64_t seg_key = sc.has_media ? rng.next() : 0ull;
       float t;
       int face;
-      const int32_t k = hit_world_nw<LDS_NODES, LDS_OBJS>(sc, o, d, time, seg_key, t, face);
+      const int32_t k = GRID ? hit_world_nw_grid(sc, o, d, time, seg_key, t, face)
+                             : hit_world_nw<LDS_NODES, LDS_OBJS>(sc, o, d, time, seg_key, t, face);
+#if RTMI_NW_PHASES
+      pb = __builtin_amdgcn_s_memtime();
+#endif
       if (k < 0) {  // background main.cu:92-99
         col = mk(T.x * sc.bg[0], T.y * sc.bg[1], T.z * sc.bg[2]);
         done = true;
@@ -165,6 +199,12 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
         }
       }
     }
+#if RTMI_NW_PHASES
+    const unsigned long long pc = __builtin_amdgcn_s_memtime();
+    pb = __shfl(pb, __builtin_ctzll(__ballot(active)));  // (set by the lanes that ran the hit)
+    ph[0] += pb - pa;
+    ph[1] += pc - pb;
+#endif
     const unsigned long long m = __ballot(done);
     if (m) {
       if (done) {
@@ -178,7 +218,15 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
       }
       next += __popcll(m);
     }
+#if RTMI_NW_PHASES
+    ph[2] += __builtin_amdgcn_s_memtime() - pc;
+#endif
   }
+#if RTMI_NW_PHASES
+  ph[3] = __builtin_amdgcn_s_memtime() - p_start;
+  if (lane == __builtin_ctzll(__ballot(1)))
+    for (int q = 0; q < 4; ++q) atomicAdd(&g_nw_phase[q], ph[q]);
+#endif
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   if (lane < nv) {
@@ -200,7 +248,7 @@ __device__ __forceinline__ void add_segments(unsigned nseg, int lane, unsigned l
   if (lane == 0) atomicAdd(segments, ws);
 }
 
-template <bool CHUNKED, bool LDS_NODES, bool LDS_OBJS>
+template <bool CHUNKED, bool LDS_NODES, bool LDS_OBJS, bool GRID>
 __global__ __launch_bounds__(64 * kWaves) void render_kernel(View sc, Args a, unsigned long long *__restrict__ accum,
                                                              float *__restrict__ out,
                                                              unsigned long long *__restrict__ segments) {
@@ -208,14 +256,14 @@ __global__ __launch_bounds__(64 * kWaves) void render_kernel(View sc, Args a, un
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * kWaves + wave;
-  stage_scene<LDS_NODES, LDS_OBJS>(sc);  // block barrier inside: before any wave leaves
+  stage_scene<LDS_NODES, LDS_OBJS, GRID>(sc);  // block barrier inside: before any wave leaves
   if (item >= a.n_items) return;         // wave-uniform
   unsigned nseg = 0;
-  run_item<CHUNKED, LDS_NODES, LDS_OBJS>(sc, a, item, lane, acc[wave], accum, out, nseg);
+  run_item<CHUNKED, LDS_NODES, LDS_OBJS, GRID>(sc, a, item, lane, acc[wave], accum, out, nseg);
   add_segments(nseg, lane, segments);
 }
 
-template <bool CHUNKED, bool LDS_OBJS>
+template <bool CHUNKED, bool LDS_OBJS, bool GRID>
 __global__ __launch_bounds__(64 * kPWaves) void render_persistent(View sc, Args a,
                                                                   unsigned long long *__restrict__ accum,
                                                                   float *__restrict__ out,
@@ -224,14 +272,14 @@ __global__ __launch_bounds__(64 * kPWaves) void render_persistent(View sc, Args 
   __shared__ unsigned long long acc[kPWaves][3][64];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  stage_scene<true, LDS_OBJS>(sc);
+  stage_scene<true, LDS_OBJS, GRID>(sc);
   unsigned nseg = 0;
   for (;;) {  // every wave leaves when the counter passes n_items
     unsigned it = 0;
     if (lane == 0) it = atomicAdd(counter, 1u);
     it = __builtin_amdgcn_readfirstlane(__shfl(it, 0));
     if (int(it) >= a.n_items) break;
-    run_item<CHUNKED, true, LDS_OBJS>(sc, a, int(it), lane, acc[wave], accum, out, nseg);
+    run_item<CHUNKED, true, LDS_OBJS, GRID>(sc, a, int(it), lane, acc[wave], accum, out, nseg);
   }
   add_segments(nseg, lane, segments);
 }
@@ -311,6 +359,14 @@ struct rt_nw_ctx {
   Image *imgd = nullptr;
   float4 *nodes = nullptr;  // 2 * nnodes: lo[] then hi[]
   int32_t nobj = 0, nnodes = 0, ninst = 0, nmat = 0, ntex = 0;
+  // uniform grid: descriptor, global arrays, brute-force list
+  bool grid_ok = false;
+  GridDesc grid{};
+  int32_t grid_max_cell = 0;
+  uint16_t *grid_cells = nullptr, *grid_refs = nullptr;
+  int32_t *grid_big = nullptr;
+  int32_t nbig = 0;
+  int32_t accel = RT_NW_ACCEL_AUTO;
   float bg[3] = {0.f, 0.f, 0.f};
   int32_t has_media = 0;
   unsigned long long *accum = nullptr;
@@ -381,6 +437,9 @@ View view_of(const rt_nw_ctx *c) {
   v.nnodes = c->nnodes;
   for (int i = 0; i < 3; ++i) v.bg[i] = c->bg[i];
   v.has_media = c->has_media;
+  v.grid = c->grid;
+  v.gbig = c->grid_big;
+  v.nbig = c->nbig;
   return v;
 }
 
@@ -406,7 +465,7 @@ RTMI_EXPORT int rt_nw_ctx_create(int32_t device, rt_nw_ctx **out) {
   if (int rc = alloc_copy<unsigned>(&ctx->counter, nullptr, 1)) return rc;
   {
     int per_cu = 0;  // the persistent grid: what stays resident (VGPR-limited: one 16-wave block per CU)
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<true, false>,
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<true, false, false>,
                                                          64 * kPWaves, 0));
     ctx->persist_blocks = per_cu * prop.multiProcessorCount;
   }
@@ -420,7 +479,8 @@ RTMI_EXPORT int rt_nw_ctx_destroy(rt_nw_ctx *ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   for (void *p : {(void *)ctx->obj, (void *)ctx->obj_id, (void *)ctx->med, (void *)ctx->med_id, (void *)ctx->inst, (void *)ctx->mat, (void *)ctx->tex,
                   (void *)ctx->pvec, (void *)ctx->pperm, (void *)ctx->img, (void *)ctx->imgd, (void *)ctx->nodes,
-                  (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments, (void *)ctx->counter})
+                  (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments, (void *)ctx->counter,
+                  (void *)ctx->grid_cells, (void *)ctx->grid_refs, (void *)ctx->grid_big})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(ctx->stream);
   if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
@@ -492,6 +552,35 @@ RTMI_EXPORT int rt_nw_ctx_set_scene(rt_nw_ctx *ctx, rt_nw_scene *s) {
       (rc = alloc_copy(&ctx->imgd, ds.image.data(), ds.image.size())) ||
       (rc = alloc_copy(&ctx->nodes, split.data(), split.size())))
     return rc;
+  ctx->grid_ok = ds.grid_ok;
+  if (ds.grid_ok) {
+    if ((rc = alloc_copy(&ctx->grid_cells, ds.grid_cell_start.data(), ds.grid_cell_start.size())) ||
+        (rc = alloc_copy(&ctx->grid_refs, ds.grid_refs.data(), ds.grid_refs.size())) ||
+        (rc = alloc_copy(&ctx->grid_big, ds.grid_big.data(), ds.grid_big.size())))
+      return rc;
+    GridDesc &G = ctx->grid;
+    for (int a = 0; a < 3; ++a) {
+      G.g0[a] = ds.grid_g0[a];
+      G.h[a] = ds.grid_h[a];
+      G.inv_h[a] = ds.grid_inv_h[a];
+      G.g1[a] = ds.grid_g1[a];
+      G.n[a] = ds.grid_n[a];
+    }
+    G.ncells = int32_t(ds.grid_cell_start.size()) - 1;
+    G.nrefs = int32_t(ds.grid_refs.size());
+    G.cell_start = ctx->grid_cells;
+    G.refs = ctx->grid_refs;
+    ctx->nbig = int32_t(ds.grid_big.size());
+    ctx->grid_max_cell = ds.grid_max_cell;
+    for (uint16_t r : ds.grid_refs)
+      if (r >= ds.obj.size()) return set_error(RT_EINVAL, "rt_nw: grid reference out of range");
+    for (int32_t b : ds.grid_big)
+      if (b < 0 || size_t(b) >= ds.obj.size()) return set_error(RT_EINVAL, "rt_nw: brute-force index out of range");
+  } else {
+    ctx->grid = GridDesc{};
+    ctx->nbig = 0;
+    ctx->grid_max_cell = 0;
+  }
   ctx->nobj = int32_t(ds.obj.size());
   ctx->nmed = int32_t(ds.med.size());
   ctx->nnodes = int32_t(ds.nodes.size());
@@ -507,6 +596,39 @@ RTMI_EXPORT int rt_nw_ctx_info(rt_nw_ctx *ctx, int32_t *n_prims, int32_t *n_node
   if (!ctx) return set_error(RT_EINVAL, "null ctx");
   if (n_prims) *n_prims = ctx->nobj + ctx->nmed;
   if (n_nodes) *n_nodes = ctx->nnodes;
+  return RT_OK;
+}
+
+namespace {
+// The structure a render uses (RT_NW_ACCEL_BVH or _GRID) and whether its
+// grid fits the LDS of the persistent / grid kernel shapes.
+constexpr int32_t kNwGridMaxCell = 24;  // AUTO: a grid with a fuller cell renders with the BVH
+size_t grid_bytes(const rt_nw_ctx *c) {
+  return nw_grid_lds_bytes(c->nobj, c->grid.ncells, c->grid.nrefs, c->nbig);
+}
+int32_t accel_used(const rt_nw_ctx *c) {
+  const bool fits = c->grid_ok && grid_bytes(c) <= kPLdsBudget;
+  if (c->accel == RT_NW_ACCEL_GRID) return fits ? RT_NW_ACCEL_GRID : RT_NW_ACCEL_BVH;
+  if (c->accel == RT_NW_ACCEL_BVH) return RT_NW_ACCEL_BVH;
+  return fits && c->grid_max_cell <= kNwGridMaxCell ? RT_NW_ACCEL_GRID : RT_NW_ACCEL_BVH;
+}
+}  // namespace
+
+RTMI_EXPORT int rt_nw_ctx_set_accel(rt_nw_ctx *ctx, int32_t accel) {
+  if (!ctx) return set_error(RT_EINVAL, "null ctx");
+  if (accel != RT_NW_ACCEL_AUTO && accel != RT_NW_ACCEL_BVH && accel != RT_NW_ACCEL_GRID)
+    return set_error(RT_EINVAL, "rt_nw_ctx_set_accel: unknown structure %d", accel);
+  ctx->accel = accel;
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_nw_ctx_accel_info(rt_nw_ctx *ctx, int32_t *accel, int32_t *dims3, int32_t *max_cell, int32_t *n_big) {
+  if (!ctx) return set_error(RT_EINVAL, "null ctx");
+  if (accel) *accel = accel_used(ctx);
+  if (dims3)
+    for (int a = 0; a < 3; ++a) dims3[a] = ctx->grid_ok ? ctx->grid.n[a] : 0;
+  if (max_cell) *max_cell = ctx->grid_ok ? ctx->grid_max_cell : 0;
+  if (n_big) *n_big = ctx->grid_ok ? ctx->nbig : 0;
   return RT_OK;
 }
 
@@ -539,7 +661,10 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
   a.tiles = a.tiles_x * ((valid + 7) / 8);
   // kernel shape: persistent when the nodes fit one CU's LDS budget, else grid
   const size_t node_bytes = size_t(ctx->nnodes) * 32, obj_bytes = size_t(ctx->nobj) * (sizeof(DevObj) + 4);
-  const bool persist = RTMI_NW_PERSIST && ctx->nnodes > 0 && node_bytes <= kPLdsBudget && ctx->persist_blocks > 0;
+  const bool use_grid = accel_used(ctx) == RT_NW_ACCEL_GRID;
+  const size_t gbytes = use_grid ? grid_bytes(ctx) : 0;
+  const bool persist = RTMI_NW_PERSIST && ctx->persist_blocks > 0 &&
+                       (use_grid || (ctx->nnodes > 0 && node_bytes <= kPLdsBudget));
   // samples per work item (same image for any size; RTMI_NW_CHUNK overrides,
   // for A/B).  Persistent kernel: ~80 items per resident wave, 4..32 samples:
   // the final scene (fog, lights: long and uneven paths) at 256 spp runs 329
@@ -569,25 +694,32 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
   HIP_TRY(hipMemsetAsync(ctx->segments, 0, sizeof(unsigned long long), st));
   const View v = view_of(ctx);
   const bool p_objs = RTMI_NW_LDS_OBJS && persist && node_bytes + obj_bytes <= kPLdsBudget;
-  const bool lds_nodes = !persist && ctx->nnodes > 0 && node_bytes <= kLdsBudget,
+  const bool g_grid = use_grid && !persist && gbytes <= kLdsBudget;  // grid kernel with the grid staged per block
+  if (use_grid && !persist && !g_grid) return set_error(RT_EINVAL, "rt_nw: grid does not fit the grid kernel's LDS");
+  const bool lds_nodes = !persist && !use_grid && ctx->nnodes > 0 && node_bytes <= kLdsBudget,
              lds_objs = RTMI_NW_LDS_OBJS && lds_nodes && node_bytes + obj_bytes <= kLdsBudget;
-  const size_t lds = persist ? (p_objs ? node_bytes + obj_bytes : node_bytes)
-                             : lds_objs ? node_bytes + obj_bytes : lds_nodes ? node_bytes : 0;
+  const size_t lds = use_grid ? gbytes
+                     : persist ? (p_objs ? node_bytes + obj_bytes : node_bytes)
+                               : lds_objs ? node_bytes + obj_bytes : lds_nodes ? node_bytes : 0;
   const unsigned blocks = persist ? unsigned(std::min<int64_t>(ctx->persist_blocks, (a.n_items + kPWaves - 1) / kPWaves))
                                   : unsigned((a.n_items + kWaves - 1) / kWaves);
   if (persist) HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
   auto launch = [&](auto chunked) {
     constexpr bool C = decltype(chunked)::value;
-    if (persist && p_objs)
-      hipLaunchKernelGGL((render_persistent<C, true>), dim3(blocks), dim3(64 * kPWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments, ctx->counter);
+    if (persist && use_grid)
+      hipLaunchKernelGGL((render_persistent<C, true, true>), dim3(blocks), dim3(64 * kPWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments, ctx->counter);
+    else if (persist && p_objs)
+      hipLaunchKernelGGL((render_persistent<C, true, false>), dim3(blocks), dim3(64 * kPWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments, ctx->counter);
     else if (persist)
-      hipLaunchKernelGGL((render_persistent<C, false>), dim3(blocks), dim3(64 * kPWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments, ctx->counter);
+      hipLaunchKernelGGL((render_persistent<C, false, false>), dim3(blocks), dim3(64 * kPWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments, ctx->counter);
+    else if (g_grid)
+      hipLaunchKernelGGL((render_kernel<C, false, false, true>), dim3(blocks), dim3(64 * kWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments);
     else if (lds_objs)
-      hipLaunchKernelGGL((render_kernel<C, true, true>), dim3(blocks), dim3(64 * kWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments);
+      hipLaunchKernelGGL((render_kernel<C, true, true, false>), dim3(blocks), dim3(64 * kWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments);
     else if (lds_nodes)
-      hipLaunchKernelGGL((render_kernel<C, true, false>), dim3(blocks), dim3(64 * kWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments);
+      hipLaunchKernelGGL((render_kernel<C, true, false, false>), dim3(blocks), dim3(64 * kWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments);
     else
-      hipLaunchKernelGGL((render_kernel<C, false, false>), dim3(blocks), dim3(64 * kWaves), 0, st, v, a, ctx->accum, dev_strip, ctx->segments);
+      hipLaunchKernelGGL((render_kernel<C, false, false, false>), dim3(blocks), dim3(64 * kWaves), 0, st, v, a, ctx->accum, dev_strip, ctx->segments);
   };
   if (a.nch > 1) {
     const size_t nv = size_t(valid) * W * 3;
@@ -649,6 +781,24 @@ RTMI_EXPORT int rt_nw_debug_trace(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
   (void)hipFree(d_n);
   if (e != hipSuccess) return set_error(RT_EHIP, "rt_nw_debug_trace: %s", hipGetErrorString(e));
   return RT_OK;
+}
+
+// Analysis builds only (RTMI_NW_PHASES): the phase cycle sums since the last
+// call (see g_nw_phase), zeroed after reading; RT_EUNSUPPORTED otherwise.
+RTMI_EXPORT int rt_nw_debug_phases(uint64_t *out4) {
+#if RTMI_NW_PHASES
+  if (!out4) return set_error(RT_EINVAL, "null");
+  HIP_TRY(hipDeviceSynchronize());
+  unsigned long long v[4];
+  HIP_TRY(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_nw_phase), sizeof v));
+  for (int q = 0; q < 4; ++q) out4[q] = v[q];
+  const unsigned long long z[4] = {0, 0, 0, 0};
+  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_nw_phase), z, sizeof z));
+  return RT_OK;
+#else
+  (void)out4;
+  return set_error(RT_EUNSUPPORTED, "rt_nw_debug_phases: not an RTMI_NW_PHASES build");
+#endif
 }
 
 RTMI_EXPORT int rt_nw_ctx_last_segments(rt_nw_ctx *ctx, uint64_t *segments) {

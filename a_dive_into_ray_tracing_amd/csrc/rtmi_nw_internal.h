@@ -37,10 +37,21 @@ struct DeviceScene {
   std::vector<Node> nodes;
   float background[3];
   bool has_media;
+  // uniform grid over the same objects; grid_ok false when
+  // the scene has none (no small objects, or it would not fit in LDS)
+  bool grid_ok = false;
+  float grid_g0[3], grid_h[3], grid_inv_h[3], grid_g1[3];
+  int32_t grid_n[3];
+  int32_t grid_max_cell = 0;               // largest cell's object count
+  std::vector<uint16_t> grid_cell_start;   // ncells + 1
+  std::vector<uint16_t> grid_refs;         // object indices (leaf order) per cell
+  std::vector<int32_t> grid_big;           // objects tested brute force beside the grid (leaf order)
 };
 
 // Flatten the world and build the BVH (RT_OK or RT_E*).
 int build_device_scene(rt_nw_scene *s, DeviceScene &out);
+// rt_nw_scene_grid_stats: the grid of build_device_scene, host only.
+int scene_grid_stats(rt_nw_scene *s, int32_t *dims3, int32_t *max_cell, int32_t *n_big, int32_t *n_refs);
 
 }  // namespace nw
 }  // namespace rtmi

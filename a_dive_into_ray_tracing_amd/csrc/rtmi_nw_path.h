@@ -120,6 +120,12 @@ struct View {
   int32_t nnodes;
   float bg[3];
   int32_t has_media;
+  // uniform grid over the objects (RT_NW_ACCEL_GRID): its
+  // descriptor (cell_start / refs: global copies) and the objects tested
+  // brute force beside it (leaf-order slots)
+  GridDesc grid;
+  const int32_t *gbig;
+  int32_t nbig;
 };
 
 __device__ __forceinline__ float4 ld4(const float (&g)[4]) { return make_float4(g[0], g[1], g[2], g[3]); }
@@ -354,6 +360,118 @@ __device__ __forceinline__ int32_t hit_world_nw(const View &sc, V o, V d, float 
       }
     }
     node = enter ? node + 1 : __float_as_int(lo.w);
+  }
+  return best;
+}
+
+// Grid LDS layout (dynamic shared memory, staged per block): the objects
+// (3 float4 each) and their insertion indices, then ncells + 1 uint16 cell
+// starts and nrefs uint16 refs (leaf-order slots), then the brute-force
+// list (int32, 4-byte aligned).
+__host__ __device__ constexpr size_t nw_grid_lds_bytes(int32_t nobj, int32_t ncells, int32_t nrefs, int32_t nbig) {
+  return size_t(nobj) * 52 + ((size_t(ncells) + 1 + size_t(nrefs)) * 2 + 3) / 4 * 4 + size_t(nbig) * 4;
+}
+
+// Closest hit through the uniform grid (RT_NW_ACCEL_GRID): the media first
+// (as hit_world_nw), then the brute-force list, then a 3D-DDA walk over the
+// cells the ray crosses inside [0, best_t], testing each cell's objects with
+// hit_object and the same order-independent (t, insertion index) rule.  The
+// walk stops at the first cell whose exit is at or beyond the closest hit so
+// far.  Exact for the reasons of the RTIOW grid: an
+// object's hit point — world ray at its t, up to the float error of an
+// instance transform — lies inside its box grown by its margin (>= 1e-3 of
+// its coordinate scale), so inside a cell that lists it; an object listed in
+// several cells gives the same t each time.  The objects' boxes cover the
+// whole shutter (moving spheres) and the composed transform (instances).
+__device__ __forceinline__ int32_t hit_world_nw_grid(const View &sc, V o, V d, float time, uint64_t seg_key,
+                                                     float &best_t, int &best_face) {
+  const DevObj *objs = reinterpret_cast<const DevObj *>(nw_nodes_lds);
+  const int32_t *oids = reinterpret_cast<const int32_t *>(nw_nodes_lds + 3 * sc.nobj);
+  const uint16_t *cs = reinterpret_cast<const uint16_t *>(oids + sc.nobj);
+  const GridDesc &G = sc.grid;
+  const uint16_t *refs = cs + G.ncells + 1;
+  const int32_t *big = reinterpret_cast<const int32_t *>(
+      reinterpret_cast<const char *>(cs) + ((size_t(G.ncells) + 1 + size_t(G.nrefs)) * 2 + 3) / 4 * 4);
+  best_t = INFINITY;
+  int32_t best = -1, best_id = 0x7fffffff;
+  best_face = -1;
+  uint32_t med_hit = 0;
+  for (int32_t m = 0; m < sc.nmed; ++m) {
+    const Obj ob = sc.med[m];
+    const int32_t id = sc.med_id[m];
+    V lo = o, ld = d;
+    if (ob.inst >= 0) to_local(sc.inst[ob.inst], lo, ld);
+    float t;
+    if (hit_medium(ob, id, lo, ld, d, time, seg_key, t) && !(t < 0.001f)) {
+      med_hit |= 1u << m;
+      if (t < best_t || (t == best_t && id < best_id)) {
+        best_t = t;
+        best = sc.nobj + m;
+        best_id = id;
+      }
+    }
+  }
+  auto test = [&](int32_t k) {
+    const DevObj ob = objs[k];
+    const int twin = ob.ka >> 8;
+    if (twin > 0 && ((med_hit >> (twin - 1)) & 1u)) return;  // hidden by its medium
+    const int32_t id = oids[k];
+    float t;
+    int face = -1;
+    if (hit_object(sc, ob, o, d, time, t, face) && (t < best_t || (t == best_t && id < best_id))) {
+      best_t = t;
+      best = k;
+      best_id = id;
+      best_face = face;
+    }
+  };
+  for (int32_t b = 0; b < sc.nbig; ++b) test(big[b]);
+  const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
+  const float ox = -o.x * ix, oy = -o.y * iy, oz = -o.z * iz;
+  const float bx0 = __builtin_fmaf(G.g0[0], ix, ox), bx1 = __builtin_fmaf(G.g1[0], ix, ox);
+  const float by0 = __builtin_fmaf(G.g0[1], iy, oy), by1 = __builtin_fmaf(G.g1[1], iy, oy);
+  const float bz0 = __builtin_fmaf(G.g0[2], iz, oz), bz1 = __builtin_fmaf(G.g1[2], iz, oz);
+  const float tnear = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(bx0, bx1), __builtin_fminf(by0, by1)),
+                                      __builtin_fmaxf(__builtin_fminf(bz0, bz1), 0.0f));
+  const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(bx0, bx1), __builtin_fmaxf(by0, by1)),
+                                     __builtin_fminf(__builtin_fmaxf(bz0, bz1), best_t));
+  if (tnear <= tfar) {
+    auto cell_of = [&](float p, int ax) {
+      const int c = int(__builtin_floorf((p - G.g0[ax]) * G.inv_h[ax]));
+      return c < 0 ? 0 : (c >= G.n[ax] ? G.n[ax] - 1 : c);
+    };
+    int cx = cell_of(__builtin_fmaf(tnear, d.x, o.x), 0);
+    int cy = cell_of(__builtin_fmaf(tnear, d.y, o.y), 1);
+    int cz = cell_of(__builtin_fmaf(tnear, d.z, o.z), 2);
+    const int sx = d.x >= 0.0f ? 1 : -1, sy = d.y >= 0.0f ? 1 : -1, sz = d.z >= 0.0f ? 1 : -1;
+    auto tface = [&](int c, int s, int ax, float inv, float oo) {
+      return __builtin_fmaf(__builtin_fmaf(float(c + (s > 0)), G.h[ax], G.g0[ax]), inv, oo);
+    };
+    float tnx = tface(cx, sx, 0, ix, ox), tny = tface(cy, sy, 1, iy, oy), tnz = tface(cz, sz, 2, iz, oz);
+    int cell = cx + G.n[0] * (cy + G.n[1] * cz);
+    const int dcx = sx, dcy = sy * G.n[0], dcz = sz * G.n[0] * G.n[1];
+    for (;;) {
+      const int e = cs[cell + 1];
+      for (int r = cs[cell]; r < e; ++r) test(int32_t(refs[r]));
+      const float texit = __builtin_fminf(tnx, __builtin_fminf(tny, tnz));
+      if (!(texit < best_t)) break;  // the closest hit so far lies in the cells walked
+      if (tnx <= tny && tnx <= tnz) {
+        cx += sx;
+        if (unsigned(cx) >= unsigned(G.n[0])) break;
+        cell += dcx;
+        tnx = tface(cx, sx, 0, ix, ox);
+      } else if (tny <= tnz) {
+        cy += sy;
+        if (unsigned(cy) >= unsigned(G.n[1])) break;
+        cell += dcy;
+        tny = tface(cy, sy, 1, iy, oy);
+      } else {
+        cz += sz;
+        if (unsigned(cz) >= unsigned(G.n[2])) break;
+        cell += dcz;
+        tnz = tface(cz, sz, 2, iz, oz);
+      }
+    }
   }
   return best;
 }

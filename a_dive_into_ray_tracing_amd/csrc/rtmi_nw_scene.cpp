@@ -5,6 +5,7 @@
 // curand XORWOW restatement they draw from.  No device code.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -436,6 +437,95 @@ struct ObjBvh {
   }
 };
 
+// Uniform grid over the non-media objects, the RTIOW grid's
+// build (rtmi_device.hip build_grid) for general objects: an object whose box
+// is more than 8x the median's largest extent (the R = 1000 ground, a
+// room-sized light) is tested brute force beside the grid; the others are
+// listed in every cell their margin-grown box overlaps.  Cell boundaries are
+// the float values g0 + c*h the device computes (origin rounded down, size
+// rounded up, so the float cells cover the box).  `order` maps leaf-order
+// slots to flattened objects; refs hold leaf-order slots.
+void build_obj_grid(const std::vector<Bounds> &bounds, const std::vector<double> &margin,
+                    const std::vector<int32_t> &order, DeviceScene &out) {
+  out.grid_ok = false;
+  const int n = int(order.size());
+  if (n == 0 || n > 65535) return;
+  std::vector<double> ext(n);
+  for (int k = 0; k < n; ++k) {
+    const Bounds &b = bounds[order[k]];
+    double e = 0;
+    for (int a = 0; a < 3; ++a) e = std::max(e, b.hi[a] - b.lo[a]);
+    ext[k] = e + 2 * margin[order[k]];
+  }
+  std::vector<double> sorted = ext;
+  std::nth_element(sorted.begin(), sorted.begin() + n / 2, sorted.end());
+  const double big_ext = 8.0 * std::max(sorted[n / 2], 1e-9);
+  std::vector<int32_t> small;
+  out.grid_big.clear();
+  for (int k = 0; k < n; ++k) (ext[k] > big_ext ? out.grid_big : small).push_back(k);
+  if (small.empty()) return;
+  auto grown = [&](int k, int a, bool hi) {
+    const Bounds &b = bounds[order[k]];
+    return hi ? b.hi[a] + margin[order[k]] : b.lo[a] - margin[order[k]];
+  };
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int32_t k : small)
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = std::min(lo[a], grown(k, a, false));
+      hi[a] = std::max(hi[a], grown(k, a, true));
+    }
+  const char *env = std::getenv("RTMI_NW_GRID_CELLS");
+  // cells per object: motion-blur scene 0.25 -> 134.1 ms, 0.5 -> 118.1, 1 -> 104.6, 2 -> 113.1,
+  // 4 -> 118.7 (BVH 114.0; profiles/r02/nw_grid/)
+  const double per_obj = env && std::atof(env) > 0 ? std::atof(env) : 1.0;
+  double e[3], vol = 1;
+  for (int a = 0; a < 3; ++a) {
+    e[a] = std::max(hi[a] - lo[a], 1e-6 * (1 + std::fabs(lo[a])));
+    vol *= e[a];
+  }
+  const double cell = std::cbrt(vol / (per_obj * double(small.size())));
+  int64_t total = 1;
+  for (int a = 0; a < 3; ++a) {
+    out.grid_n[a] = int32_t(std::min<double>(128, std::max<double>(1, std::ceil(e[a] / cell))));
+    total *= out.grid_n[a];
+  }
+  if (total > 16384) return;
+  for (int a = 0; a < 3; ++a) {
+    float g0 = float(lo[a]);
+    if (double(g0) > lo[a]) g0 = std::nextafter(g0, -INFINITY);
+    float h = float(e[a] / out.grid_n[a]);
+    while (double(g0) + double(h) * out.grid_n[a] < hi[a]) h = std::nextafter(h, INFINITY);
+    out.grid_g0[a] = g0;
+    out.grid_h[a] = h;
+    out.grid_inv_h[a] = 1.0f / h;
+    out.grid_g1[a] = std::fmaf(float(out.grid_n[a]), h, g0);
+  }
+  std::vector<std::vector<uint16_t>> lists(static_cast<size_t>(total));
+  for (int32_t k : small) {
+    int c0[3], c1[3];
+    for (int a = 0; a < 3; ++a) {  // every cell [g0 + c*h, g0 + (c+1)*h] the grown box touches
+      const double g0 = out.grid_g0[a], h = out.grid_h[a];
+      c0[a] = std::max(0, std::min(out.grid_n[a] - 1, int(std::floor((grown(k, a, false) - g0) / h))));
+      c1[a] = std::max(0, std::min(out.grid_n[a] - 1, int(std::floor((grown(k, a, true) - g0) / h))));
+    }
+    for (int z = c0[2]; z <= c1[2]; ++z)
+      for (int y = c0[1]; y <= c1[1]; ++y)
+        for (int x = c0[0]; x <= c1[0]; ++x)
+          lists[size_t(x + out.grid_n[0] * (y + out.grid_n[1] * z))].push_back(uint16_t(k));
+  }
+  out.grid_cell_start.assign(size_t(total) + 1, 0);
+  out.grid_refs.clear();
+  out.grid_max_cell = 0;
+  for (int64_t c = 0; c < total; ++c) {
+    out.grid_cell_start[size_t(c)] = uint16_t(out.grid_refs.size());
+    out.grid_refs.insert(out.grid_refs.end(), lists[size_t(c)].begin(), lists[size_t(c)].end());
+    out.grid_max_cell = std::max(out.grid_max_cell, int32_t(lists[size_t(c)].size()));
+    if (out.grid_refs.size() > 65535) return;
+  }
+  out.grid_cell_start[size_t(total)] = uint16_t(out.grid_refs.size());
+  out.grid_ok = true;
+}
+
 }  // namespace
 
 namespace rtmi {
@@ -499,6 +589,7 @@ int build_device_scene(rt_nw_scene *s, DeviceScene &out) {
     out.obj_id[k] = bvh.order[k];
     if (out.obj[k].aux > 0) out.obj[k].aux = med_index[out.obj[k].aux - 1] + 1;  // twin -> media-list index + 1
   }
+  build_obj_grid(s->flat_bounds, margin, bvh.order, out);
   out.inst = s->flat_inst;
   out.mat = s->mat;
   out.tex = s->tex;
@@ -508,6 +599,16 @@ int build_device_scene(rt_nw_scene *s, DeviceScene &out) {
   out.image = s->image;
   for (int c = 0; c < 3; ++c) out.background[c] = s->background[c];
   out.has_media = !out.med.empty();
+  return RT_OK;
+}
+
+int scene_grid_stats(rt_nw_scene *s, int32_t *dims3, int32_t *max_cell, int32_t *n_big, int32_t *n_refs) {
+  DeviceScene ds;
+  if (int rc = build_device_scene(s, ds)) return rc;
+  for (int a = 0; a < 3 && dims3; ++a) dims3[a] = ds.grid_ok ? ds.grid_n[a] : 0;
+  if (max_cell) *max_cell = ds.grid_ok ? ds.grid_max_cell : 0;
+  if (n_big) *n_big = ds.grid_ok ? int32_t(ds.grid_big.size()) : 0;
+  if (n_refs) *n_refs = ds.grid_ok ? int32_t(ds.grid_refs.size()) : 0;
   return RT_OK;
 }
 
@@ -730,6 +831,11 @@ RTMI_EXPORT int rt_nw_set_background(rt_nw_scene *s, double r, double g, double 
   s->background[1] = float(g);
   s->background[2] = float(b);
   return RT_OK;
+}
+
+RTMI_EXPORT int rt_nw_scene_grid_stats(rt_nw_scene *s, int32_t *dims3, int32_t *max_cell, int32_t *n_big,
+                                       int32_t *n_refs) {
+  return rtmi::nw::scene_grid_stats(s, dims3, max_cell, n_big, n_refs);
 }
 
 RTMI_EXPORT int rt_nw_scene_flat(rt_nw_scene *s, rt_nw_flat *out) {

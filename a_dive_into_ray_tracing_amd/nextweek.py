@@ -147,6 +147,15 @@ class Scene:
             "n_obj": f.n_obj,
         }
 
+    def grid_stats(self):
+        """The uniform grid a device context would build (host only,
+        rt_nw_scene_grid_stats): {"dims", "max_cell", "n_big", "n_refs"}."""
+        dims = (C.c_int32 * 3)()
+        mc, nb, nr = C.c_int32(), C.c_int32(), C.c_int32()
+        check(load().rt_nw_scene_grid_stats(self._h, dims, C.byref(mc), C.byref(nb), C.byref(nr)),
+              "rt_nw_scene_grid_stats")
+        return {"dims": tuple(dims), "max_cell": mc.value, "n_big": nb.value, "n_refs": nr.value}
+
     def close(self):
         if self._h:
             load().rt_nw_scene_destroy(self._h)
@@ -204,6 +213,23 @@ class NwRenderer:
         a, b = C.c_int32(), C.c_int32()
         check(load().rt_nw_ctx_info(self._h, C.byref(a), C.byref(b)), "rt_nw_ctx_info")
         return a.value, b.value
+
+    ACCELS = {"auto": 0, "bvh": 1, "grid": 2}
+
+    def set_accel(self, kind):
+        """Closest-hit structure: "auto" (the grid when balanced, else the BVH),
+        "bvh" or "grid" (rt_nw_ctx_set_accel); the same image either way."""
+        check(load().rt_nw_ctx_set_accel(self._h, self.ACCELS[kind]), "rt_nw_ctx_set_accel")
+
+    def accel_info(self):
+        """{"accel": the structure renders use, "dims": grid cells per axis
+        (zeros: no grid), "max_cell": fullest cell, "n_big": brute-force list}."""
+        used, mc, nb = C.c_int32(), C.c_int32(), C.c_int32()
+        dims = (C.c_int32 * 3)()
+        check(load().rt_nw_ctx_accel_info(self._h, C.byref(used), dims, C.byref(mc), C.byref(nb)),
+              "rt_nw_ctx_accel_info")
+        names = {v: k for k, v in self.ACCELS.items()}
+        return {"accel": names[used.value], "dims": tuple(dims), "max_cell": mc.value, "n_big": nb.value}
 
     def render(self, cam, W, H, spp, max_depth=50, seed=1984):
         out = np.zeros((H, W, 3), np.float32)

@@ -345,6 +345,8 @@ def main():
                          "kernel averages must cover only the warmup + timed launches")
     ap.add_argument("--workload", choices=list(RTIOW_WORKLOADS) + ["nw_motion_blur", "nw_final"], default="config2")
     ap.add_argument("--nw-spp", type=int, default=0, help="spp of the nw_* workloads (default: 500 / 1024)")
+    ap.add_argument("--nw-accel", choices=["auto", "bvh", "grid"], default="auto",
+                    help="closest-hit structure of the nw_* workloads (rt_nw_ctx_set_accel; same image)")
     ap.add_argument("--strip-of", type=int, default=0,
                     help="analysis only: time ONE rank's interleaved strip of an N-GPU run on this GPU")
     args = ap.parse_args()
@@ -640,6 +642,8 @@ def bench_nw(args):
         earth = nw.load_image(os.path.join(REPO, "tests", "golden", "earthmap.jpeg"))
     scene, cam = nw.preset(which, image=earth, aspect=Wn / Hn)
     r = nw.NwRenderer(scene, local_rank)
+    r.set_accel(args.nw_accel)
+    accel = r.accel_info()
     row0, row_step, nrows = rdist.strip_rows(Hn, rank, N)
     strip = torch.empty((nrows, Wn, 3), dtype=torch.float32, device=dev)
     stream = torch.cuda.Stream(dev)
@@ -692,14 +696,16 @@ def bench_nw(args):
             "data": "synthetic: the reference's scene regenerated from a restated curand XORWOW (curand_init(1984,0,0))",
             "config": {"workload": f"{args.workload}_{Wn}x{Hn}_{spp}spp_depth{DEPTH}", "scene": which, "width": Wn,
                        "height": Hn, "spp": spp, "max_depth": DEPTH, "seed": SEED,
-                       "partition": "interleaved rows, one RCCL gather" if N > 1 else "single GPU"},
+                       "partition": "interleaved rows, one RCCL gather" if N > 1 else "single GPU",
+                       "accel": accel["accel"], "grid_dims": list(accel["dims"]), "grid_max_cell": accel["max_cell"],
+                       "brute_force_objects": accel["n_big"]},
             "roofline": {
                 "bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
                 "flop_per_launch": flop_rank, "flop_per_segment": flop_seg, "segments_per_launch": segs,
                 "kernel_ms": round(kernel_ms, 3), "work_equivalent": True,
                 "note": "brute-force-equivalent FLOP (every object's miss test per world.hit, bench.NW_FLOP) over the "
-                        "BVH kernel's time, as SURVEY 8(d) prescribes for culling: frac can exceed 1",
+                        "BVH / grid kernel's time, as SURVEY 8(d) prescribes for culling: frac can exceed 1",
             },
             "kernel_ms": round(kernel_ms, 3),
             "segments_per_sample_rank0": round(segs / (nrows * Wn * spp), 4),

@@ -129,6 +129,11 @@ typedef struct rt_nw_flat {
   float background[3];
 } rt_nw_flat;
 int rt_nw_scene_flat(rt_nw_scene *s, rt_nw_flat *out);
+/* Host only (no device needed): the uniform grid rt_nw_ctx_set_scene would
+ * build for this scene — cells per axis (zeros: no grid),
+ * the fullest cell's object count, the brute-force list's length and the
+ * total cell references.  Any output may be null. */
+int rt_nw_scene_grid_stats(rt_nw_scene *s, int32_t *dims3, int32_t *max_cell, int32_t *n_big, int32_t *n_refs);
 
 /* ---- device ------------------------------------------------------------ */
 int rt_nw_ctx_create(int32_t device, rt_nw_ctx **out);
@@ -137,6 +142,22 @@ int rt_nw_ctx_destroy(rt_nw_ctx *ctx);
 int rt_nw_ctx_set_scene(rt_nw_ctx *ctx, rt_nw_scene *s);
 /* n_prims, n_nodes of the resident BVH */
 int rt_nw_ctx_info(rt_nw_ctx *ctx, int32_t *n_prims, int32_t *n_nodes);
+/* Closest-hit structure over the non-media objects (media are always tested
+ * first).  RT_NW_ACCEL_BVH: the SAH BVH (skip-link walk).
+ * RT_NW_ACCEL_GRID: a uniform grid walked by a 3D DDA, objects much larger
+ * than the median in a brute-force list beside it; offered
+ * when the scene has one (rt_nw_ctx_accel_info).  RT_NW_ACCEL_AUTO (a new
+ * context's setting): the grid when it is balanced (at most 24 objects in
+ * any cell), else the BVH.  All give the same closest hit, so the same image
+ * bit for bit.  Replaces the choice of hittable in main.cu:420-490 (the
+ * reference always wraps the world in its bvh_node). */
+enum { RT_NW_ACCEL_AUTO = 0, RT_NW_ACCEL_BVH = 1, RT_NW_ACCEL_GRID = 2 };
+int rt_nw_ctx_set_accel(rt_nw_ctx *ctx, int32_t accel);
+/* The structure renders use now (RT_NW_ACCEL_BVH or _GRID, after AUTO is
+ * resolved); the grid's cells per axis (dims3, 0 when the scene has no grid),
+ * its largest cell's object count and the brute-force list's length.  Any
+ * output may be null. */
+int rt_nw_ctx_accel_info(rt_nw_ctx *ctx, int32_t *accel_used, int32_t *dims3, int32_t *max_cell, int32_t *n_big);
 /* The whole image (main.cu:125-145 + the caller's output loop), host sums,
  * synchronous.  Pixel (i, j) samples u = (i + r)/W, v = (j + r)/H
  * (main.cu:139-140). */
@@ -154,6 +175,10 @@ int rt_nw_debug_trace(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32_t W, int32_
                       uint64_t seed, int32_t i, int32_t j, int32_t s, float *rec, int32_t cap, int32_t *n);
 /* world.hit calls of the last render (waits for it). */
 int rt_nw_ctx_last_segments(rt_nw_ctx *ctx, uint64_t *segments);
+/* Analysis builds only (-DRTMI_NW_PHASES=1): wave-level cycles of the loop
+ * passes since the last call — closest hit, hit record + texture + scatter,
+ * accumulation + regeneration, whole items; RT_EUNSUPPORTED otherwise. */
+int rt_nw_debug_phases(uint64_t *out4);
 
 #ifdef __cplusplus
 }

@@ -191,3 +191,17 @@ def test_cli_usage_without_gpu():
     assert r.returncode == 2 and "usage" in r.stderr
     r = subprocess.run([exe, "--scene", "nope"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 2 and "unknown scene" in r.stderr
+
+
+def test_grid_stats_of_presets():
+    """The uniform grid the device would build (host only):
+    the motion-blur random_scene gets a balanced grid with the R = 1000
+    ground in the brute-force list; the final scene's 1000-sphere cluster
+    fills a few cells (auto renders it with the BVH)."""
+    s, _ = nw.preset(1, aspect=1.5)
+    g = s.grid_stats()
+    assert g["n_big"] == 1 and g["max_cell"] <= 24 and min(g["dims"]) >= 1, g
+    assert g["n_refs"] >= 480  # every small object listed at least once
+    s, _ = nw.preset(8, image=np.zeros((4, 4, 3), np.uint8), aspect=1.0)
+    g = s.grid_stats()
+    assert g["max_cell"] > 24, g

@@ -28,11 +28,18 @@ def earth():
     return nw.load_image(os.path.join(GOLD, "earthmap.jpeg"))
 
 
+@pytest.mark.parametrize("accel", ["bvh", "grid"])
 @pytest.mark.parametrize("which", list(range(1, 9)))
-def test_presets_bit_exact_vs_oracle(which, earth):
+def test_presets_bit_exact_vs_oracle(which, accel, earth):
+    """Both closest-hit structures (the BVH and the uniform grid with its
+    brute-force list) against the oracle's plain list."""
     W, H, spp = 29, 23, 3  # ragged: partial 8x8 tiles on both axes
     s, cam = nw.preset(which, image=earth, aspect=W / H)
     r = nw.NwRenderer(s)
+    r.set_accel(accel)
+    info = r.accel_info()
+    if accel == "grid" and which == 1:
+        assert info["accel"] == "grid" and info["n_big"] >= 1, info  # the R = 1000 ground beside the grid
     got = r.render(cam, W, H, spp, 50, SEED)
     segs = r.last_segments()
     r.close()
@@ -42,8 +49,9 @@ def test_presets_bit_exact_vs_oracle(which, earth):
     assert segs == want_segs
 
 
-@pytest.mark.parametrize("which", [6, 7, 8])
-def test_chunked_strips_bit_exact(which, earth):
+@pytest.mark.parametrize("accel", ["bvh", "grid"])
+@pytest.mark.parametrize("which", [1, 6, 7, 8])
+def test_chunked_strips_bit_exact(which, accel, earth):
     """spp > the 32-sample item (two-item accumulation + finalize) and an
     interleaved strip of rows, through rt_nw_render_rows on a torch stream."""
     import torch
@@ -51,6 +59,7 @@ def test_chunked_strips_bit_exact(which, earth):
     W, H, spp = 24, 40, 70
     s, cam = nw.preset(which, image=earth, aspect=1.0)
     r = nw.NwRenderer(s)
+    r.set_accel(accel)
     row0, step, nrows = 1, 3, 14  # rows 1, 4, ..., 40 (the last past H: zero)
     strip = torch.full((nrows, W, 3), -1.0, dtype=torch.float32, device="cuda")
     st = torch.cuda.Stream()
@@ -141,8 +150,9 @@ def test_cli_matches_library(tmp_path, earth):
         assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("accel", ["bvh", "grid"])
 @pytest.mark.parametrize("shutter", [(0.0, 1.0), (0.3, 0.6)])
-def test_moving_spheres_bit_exact(shutter):
+def test_moving_spheres_bit_exact(shutter, accel):
     """Moving spheres with their own time ranges inside and outside the
     shutter (the centre extrapolates linearly; their BVH boxes are swept over
     [0, 1]), under translate/rotate_y instances and as a medium's boundary:
@@ -171,8 +181,70 @@ def test_moving_spheres_bit_exact(shutter):
     W, H, spp = 40, 30, 6
     cam = nw.camera((13, 2, 3), (0, 0, 0), (0, 1, 0), 30.0, W / H, 0.1, 10.0, *shutter)
     r = nw.NwRenderer(s)
+    r.set_accel(accel)
+    assert r.accel_info()["accel"] == accel
     got, segs = r.render(cam, W, H, spp, 50, SEED), r.last_segments()
     r.close()
     want, want_segs = O.nw_render(s.flat(), cam, W, H, spp, 50, SEED)
     assert np.array_equal(got, want), f"max |d| {np.abs(got - want).max()}"
+    assert segs == want_segs
+
+
+@pytest.mark.parametrize("seed", [3, 11])
+def test_grid_mixed_objects_bit_exact(seed):
+    """The grid over every object kind at once — rectangles (zero thickness)
+    in the three planes, boxes, rotated and translated instances, moving and
+    static spheres, a box-bounded medium, lights — scaled x100 and shifted
+    far from the origin (coordinates ~3000: cell faces far from 0 in float):
+    grid == oracle (brute force) and BVH == oracle, world.hit counts
+    included; auto picks the grid."""
+    g = np.random.default_rng(seed)
+    S = 100.0
+    off = np.array([3000.0, -1500.0, 2200.0])
+    s = nw.Scene()
+    gray = s.lambertian(s.solid(0.5, 0.5, 0.5))
+    mats = [gray, s.metal(s.solid(0.8, 0.7, 0.6), 0.1), s.dielectric(1.5)]
+    light = s.diffuse_light(s.solid(4, 4, 4))
+    s.add(s.sphere(tuple(off + S * np.array([0, -1000, 0])), 1000 * S, gray))
+    kids = []
+    for k in range(240):
+        inside = k % 8 == 0  # every 8th object goes into the instance: built around the origin, moved by it
+        base = np.zeros(3) if inside else off
+        P = lambda *v: tuple(base + S * np.array(v, dtype=np.float64))
+        x, y, z = g.uniform(-8, 8), g.uniform(0.1, 2.0), g.uniform(-8, 8)
+        m = mats[k % 3]
+        kind = k % 6
+        if kind == 0:
+            o = s.sphere(P(x, y, z), S * g.uniform(0.1, 0.4), m)
+        elif kind == 1:
+            o = s.moving_sphere(P(x, y, z), P(x, y + g.uniform(0, 0.5), z), 0.0, 1.0, S * g.uniform(0.1, 0.3), m)
+        elif kind == 2:
+            o = s.box(P(x, 0, z), P(x + g.uniform(0.2, 0.8), g.uniform(0.2, 1.5), z + g.uniform(0.2, 0.8)), m)
+        else:
+            plane = kind - 3  # xy, xz, yz: in-plane axes (a, b), plane axis k
+            ax_a, ax_b, ax_k = [0, 0, 1][plane], [1, 2, 2][plane], [2, 1, 0][plane]
+            lo = np.array(P(x, y, z))
+            o = s.rect(["xy", "xz", "yz"][plane], lo[ax_a], lo[ax_a] + 0.6 * S, lo[ax_b], lo[ax_b] + 0.6 * S,
+                       float(lo[ax_k]), m if k % 7 else light)
+        if inside:
+            kids.append(o)
+        else:
+            s.add(o)
+    s.add(s.translate(s.rotate_y(s.group(kids), 33.0), tuple(off + S * np.array([0.5, 0.0, -0.7]))))
+    fog_box = s.box(tuple(off + S * np.array([3, 0, 3])), tuple(off + S * np.array([4.5, 1.5, 4.5])), gray)
+    s.add(s.constant_medium(fog_box, 0.008, s.solid(0.9, 0.9, 0.9)))
+    s.set_background(0.7, 0.8, 1.0)
+    stats = s.grid_stats()
+    assert stats["n_big"] == 1 and stats["max_cell"] <= 24, stats
+    W, H, spp = 40, 30, 5
+    cam = nw.camera(tuple(off + S * np.array([13, 2, 3])), tuple(off), (0, 1, 0), 30.0, W / H, 0.1 * S, 10.0 * S)
+    r = nw.NwRenderer(s)
+    assert r.accel_info()["accel"] == "grid"
+    got, segs = r.render(cam, W, H, spp, 50, SEED), r.last_segments()
+    r.set_accel("bvh")
+    got_bvh = r.render(cam, W, H, spp, 50, SEED)
+    r.close()
+    want, want_segs = O.nw_render(s.flat(), cam, W, H, spp, 50, SEED)
+    assert np.array_equal(got, want), f"max |d| {np.abs(got - want).max()}"
+    assert np.array_equal(got_bvh, want)
     assert segs == want_segs

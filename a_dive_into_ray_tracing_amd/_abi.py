@@ -134,6 +134,7 @@ SIGNATURES = {
     "rt_nw_ctx_info": (C.c_int, [C.c_void_p, _ip, _ip]),
     "rt_nw_ctx_set_accel": (C.c_int, [C.c_void_p, C.c_int32]),
     "rt_nw_scene_grid_stats": (C.c_int, [C.c_void_p, _ip, _ip, _ip, _ip]),
+    "rt_nw_debug_phases": (C.c_int, [C.POINTER(C.c_uint64)]),
     "rt_nw_ctx_accel_info": (C.c_int, [C.c_void_p, _ip, _ip, _ip, _ip]),
     "rt_nw_render": (C.c_int, [C.c_void_p, C.POINTER(RtNwCamera)] + [C.c_int32] * 4 + [C.c_uint64, _fp]),
     "rt_nw_render_rows": (

@@ -411,7 +411,11 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
       // 1/|d| once for the lanes that need it: the sky of a miss (main.cpp:80)
       // and unit(din) of metal and dielectric — the same expression
       const bool miss = k < 0 || (RTMI_CHECK && k >= a.n);
-      const int kind = miss ? -1 : int(sc.sh1[k].x);
+      // the hit sphere's three records in one memory round trip (a miss reads
+      // sphere 0's, unused)
+      const int kk = miss ? 0 : k;
+      const float4 sh1k = sc.sh1[kk], sh0k = sc.sh0[kk], geomk = sc.geom[kk];
+      const int kind = miss ? -1 : int(sh1k.x);
       float inv_len = 0.0f;
       if (kind != RT_MAT_LAMBERTIAN) inv_len = 1.0f / dsqrt(dot<true>(d, d));
       if (miss) {
@@ -421,8 +425,8 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
       } else {
         V3<float> p, nrm, at, nd;
         bool front;
-        hit_record<true, float>(sc, k, o, d, t, p, nrm, front);
-        if (!scatter_fast(sc, k, d, nrm, front, rng, at, nd, inv_len)) {
+        hit_record_fast(geomk, sh0k.x, o, d, t, p, nrm, front);
+        if (!scatter_fast(sh0k, sh1k, d, nrm, front, rng, at, nd, inv_len)) {
           done = true;  // absorbed (metal below the surface): black, main.cpp:78
         } else {
           T = mk(T.x * at.x, T.y * at.y, T.z * at.z);
@@ -810,7 +814,11 @@ __global__ __launch_bounds__(64 * PersistShape<ACC>::waves, PersistShape<ACC>::p
       // 1/|d| once for the lanes that need it: the sky of a miss (main.cpp:80)
       // and unit(din) of metal and dielectric — the same expression
       const bool miss = k < 0 || (RTMI_CHECK && k >= a.n);
-      const int kind = miss ? -1 : int(sc.sh1[k].x);
+      // the hit sphere's three records in one memory round trip (a miss reads
+      // sphere 0's, unused)
+      const int kk = miss ? 0 : k;
+      const float4 sh1k = sc.sh1[kk], sh0k = sc.sh0[kk], geomk = sc.geom[kk];
+      const int kind = miss ? -1 : int(sh1k.x);
       float inv_len = 0.0f;
       if (kind != RT_MAT_LAMBERTIAN) inv_len = 1.0f / dsqrt(dot<true>(d, d));
       if (miss) {
@@ -820,8 +828,8 @@ __global__ __launch_bounds__(64 * PersistShape<ACC>::waves, PersistShape<ACC>::p
       } else {
         V3<float> p, nrm, at, nd;
         bool front;
-        hit_record<true, float>(sc, k, o, d, t, p, nrm, front);
-        if (!scatter_fast(sc, k, d, nrm, front, rng, at, nd, inv_len)) {
+        hit_record_fast(geomk, sh0k.x, o, d, t, p, nrm, front);
+        if (!scatter_fast(sh0k, sh1k, d, nrm, front, rng, at, nd, inv_len)) {
           done = true;
         } else {
           T = mk(T.x * at.x, T.y * at.y, T.z * at.z);

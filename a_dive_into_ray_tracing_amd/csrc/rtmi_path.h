@@ -650,6 +650,15 @@ struct Accel {
   GridDesc grid;             // RT_ACCEL_GRID only
 };
 
+__device__ __forceinline__ int32_t big_index(const Accel &a, int slot) {
+#if RTMI_BIG_SCALAR
+  typedef const __attribute__((address_space(4))) int32_t *cidx_t;
+  return ((cidx_t)(size_t)a.big_idx)[slot];
+#else
+  return a.big_idx[slot];
+#endif
+}
+
 // The BVH lives in LDS during a launch (dynamic shared memory, staged by
 // every block at its start): the traversal is a chain of dependent node
 // loads, ~100 cycles from LDS against ~500+ from L2.  Layout: nnodes 16-byte
@@ -674,6 +683,11 @@ __device__ __forceinline__ void stage_bvh(const Accel &g) {
 // < 65536 refs).
 #ifndef RTMI_BIG_LDS
 #define RTMI_BIG_LDS 0
+#endif
+// RTMI_BIG_SCALAR: the big spheres and their scene indices (wave-uniform
+// addresses) read with scalar loads through the constant address space
+#ifndef RTMI_BIG_SCALAR
+#define RTMI_BIG_SCALAR 1
 #endif
 constexpr int kBigLdsPairs = 4;  // big-sphere pairs staged after the grid (RTMI_BIG_LDS)
 __host__ __device__ constexpr size_t grid_lds_bytes(int32_t nsph, int32_t ncells, int32_t nrefs) {
@@ -793,6 +807,13 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
 #pragma unroll
         for (int g = 0; g < GP; ++g) p[g] = acc_s.big[q + g];
       }
+#elif RTMI_BIG_SCALAR
+      // uniform addresses through the constant address space: scalar loads
+      // (s_load, scalar cache) instead of per-lane vector loads
+      typedef const __attribute__((address_space(4))) SpherePair *cpair_t;
+      const cpair_t cp = (cpair_t)(size_t)acc_s.big;
+#pragma unroll
+      for (int g = 0; g < GP; ++g) { p[g].cx = cp[q + g].cx; p[g].cy = cp[q + g].cy; p[g].cz = cp[q + g].cz; p[g].S = cp[q + g].S; }
 #else
 #pragma unroll
       for (int g = 0; g < GP; ++g) p[g] = acc_s.big[q + g];
@@ -814,8 +835,8 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
       if (any < 0) {
 #pragma unroll
         for (int g = 0; g < GP; ++g) {
-          if (ci[2 * g] < 0) resolve(acc_s.big_idx[2 * (q + g)], hb[g].x, disc[g].x);
-          if (ci[2 * g + 1] < 0) resolve(acc_s.big_idx[2 * (q + g) + 1], hb[g].y, disc[g].y);
+          if (ci[2 * g] < 0) resolve(big_index(acc_s, 2 * (q + g)), hb[g].x, disc[g].x);
+          if (ci[2 * g + 1] < 0) resolve(big_index(acc_s, 2 * (q + g) + 1), hb[g].y, disc[g].y);
         }
       }
     }
@@ -993,8 +1014,8 @@ __device__ __forceinline__ int32_t hit_world_bvh(const Accel &acc_s, V3<float> o
       if (any < 0) {
 #pragma unroll
         for (int g = 0; g < GP; ++g) {
-          if (ci[2 * g] < 0) resolve(acc_s.big_idx[2 * (q + g)], hb[g].x, disc[g].x);
-          if (ci[2 * g + 1] < 0) resolve(acc_s.big_idx[2 * (q + g) + 1], hb[g].y, disc[g].y);
+          if (ci[2 * g] < 0) resolve(big_index(acc_s, 2 * (q + g)), hb[g].x, disc[g].x);
+          if (ci[2 * g + 1] < 0) resolve(big_index(acc_s, 2 * (q + g) + 1), hb[g].y, disc[g].y);
         }
       }
     }
@@ -1113,10 +1134,10 @@ __device__ __forceinline__ bool scatter(const SceneView<R> &sc, int32_t k, V3<R>
 // generator state back.
 // inv_len = 1/sqrt(din.din) (correctly rounded), as unit() computes it; the
 // caller shares it with the sky of the wave's missed lanes.
-__device__ __forceinline__ bool scatter_fast(const SceneView<float> &sc, int32_t k, V3<float> din, V3<float> normal,
+// (s0, s1 = shade0[k], shade1[k]: the caller loads the hit sphere's records
+// together, in one memory round trip)
+__device__ __forceinline__ bool scatter_fast(const float4 s0, const float4 s1, V3<float> din, V3<float> normal,
                                              bool front, Xoro &g, V3<float> &atten, V3<float> &dout, float inv_len) {
-  const float4 s0 = sc.sh0[k];
-  const float4 s1 = sc.sh1[k];
   const int kind = int(s1.x);
   const Xoro g0 = g;
   float u, v;
@@ -1174,6 +1195,16 @@ __device__ __forceinline__ void hit_record(const SceneView<R> &sc, int32_t k, V3
   p = mk(madd<F>(t, d.x, o.x), madd<F>(t, d.y, o.y), madd<F>(t, d.z, o.z));  // ray::at ray.h:15
   const V3<R> outward = scale(inv_r, mk(p.x - g.x, p.y - g.y, p.z - g.z));
   front = dot<F>(d, outward) < R(0);
+  normal = front ? outward : mk(-outward.x, -outward.y, -outward.z);
+}
+
+// hit_record for the fast kernels, given the sphere's geom record g and 1/r
+// (loaded by the caller with its shade records)
+__device__ __forceinline__ void hit_record_fast(const float4 g, float inv_r, V3<float> o, V3<float> d, float t,
+                                                V3<float> &p, V3<float> &normal, bool &front) {
+  p = mk(__builtin_fmaf(t, d.x, o.x), __builtin_fmaf(t, d.y, o.y), __builtin_fmaf(t, d.z, o.z));  // ray::at ray.h:15
+  const V3<float> outward = scale(inv_r, mk(p.x - g.x, p.y - g.y, p.z - g.z));
+  front = dot<true>(d, outward) < 0.0f;
   normal = front ? outward : mk(-outward.x, -outward.y, -outward.z);
 }
 

@@ -79,6 +79,32 @@ __device__ __forceinline__ int64_t fixed(float c) {
   return int64_t(g * 4294967296.0f);
 }
 
+// The camera, shutter and image size in LDS (23 floats), read at each
+// regeneration: the kernel's scalar registers otherwise overflow and the
+// compiler parks them in VGPR lanes (v_readlane at every regeneration), as in
+// the RTIOW kernel.  Staged before stage_scene's barrier.
+#ifndef RTMI_NW_CAM_LDS
+#define RTMI_NW_CAM_LDS 1
+#endif
+__device__ __forceinline__ void stage_camera(float *cl, const Args &a) {
+  const unsigned t = threadIdx.x;
+  if (t < 23) {
+    float v;
+    switch (t / 3) {
+      case 0: v = (&a.cam.origin.x)[t % 3]; break;
+      case 1: v = (&a.cam.llc.x)[t % 3]; break;
+      case 2: v = (&a.cam.hor.x)[t % 3]; break;
+      case 3: v = (&a.cam.ver.x)[t % 3]; break;
+      case 4: v = (&a.cam.u.x)[t % 3]; break;
+      case 5: v = (&a.cam.v.x)[t % 3]; break;
+      default:
+        v = t == 18 ? a.cam.lens : t == 19 ? a.time0 : t == 20 ? a.time1 - a.time0 : t == 21 ? float(a.W) : float(a.H);
+        break;
+    }
+    cl[t] = v;
+  }
+}
+
 template <bool LDS_NODES, bool LDS_OBJS, bool GRID>
 __device__ __forceinline__ void stage_scene(const View &sc) {
   if constexpr (GRID) {  // objects, insertion indices, cell starts, refs, brute-force list (nw_grid_lds_bytes)
@@ -115,7 +141,7 @@ __device__ __forceinline__ void stage_scene(const View &sc) {
 template <bool CHUNKED, bool LDS_NODES, bool LDS_OBJS, bool GRID>
 __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item, int lane,
                                          unsigned long long (&acc)[3][64], unsigned long long *__restrict__ accum,
-                                         float *__restrict__ out, unsigned &nseg) {
+                                         float *__restrict__ out, unsigned &nseg, const float *cl) {
   const int tile = item / a.nch;
   const int s0 = (item - tile * a.nch) * a.chunk;
   const int ns = min(a.chunk, a.spp - s0);
@@ -143,10 +169,27 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
     rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(s));
     float ju, jv;
     rng.pair(ju, jv);
+#if RTMI_NW_CAM_LDS
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // read here, not hoisted out of the loop
+    const float u = (float(i) + ju) / cl[21];
+    const float v = (float(j) + jv) / cl[22];
+    Cam<float> cm;
+    cm.origin = mk(cl[0], cl[1], cl[2]);
+    cm.llc = mk(cl[3], cl[4], cl[5]);
+    cm.hor = mk(cl[6], cl[7], cl[8]);
+    cm.ver = mk(cl[9], cl[10], cl[11]);
+    cm.u = mk(cl[12], cl[13], cl[14]);
+    cm.v = mk(cl[15], cl[16], cl[17]);
+    cm.lens = cl[18];
+    get_ray<true, float>(cm, u, v, rng, o, d);
+    time = __builtin_fmaf(rng.uni(), cl[20], cl[19]);  // camera.h:75-79
+#else
+    (void)cl;
     const float u = (float(i) + ju) / float(a.W);
     const float v = (float(j) + jv) / float(a.H);
     get_ray<true, float>(a.cam, u, v, rng, o, d);
     time = __builtin_fmaf(rng.uni(), a.time1 - a.time0, a.time0);  // camera.h:75-79
+#endif
     T = mk(1.f, 1.f, 1.f);
     depth = 0;
   };
@@ -256,10 +299,13 @@ __global__ __launch_bounds__(64 * kWaves) void render_kernel(View sc, Args a, un
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * kWaves + wave;
+  __shared__ float cam_lds[23];
+  stage_camera(cam_lds, a);
+  if constexpr (!LDS_NODES && !GRID) __syncthreads();  // (stage_scene's barrier covers the others)
   stage_scene<LDS_NODES, LDS_OBJS, GRID>(sc);  // block barrier inside: before any wave leaves
   if (item >= a.n_items) return;         // wave-uniform
   unsigned nseg = 0;
-  run_item<CHUNKED, LDS_NODES, LDS_OBJS, GRID>(sc, a, item, lane, acc[wave], accum, out, nseg);
+  run_item<CHUNKED, LDS_NODES, LDS_OBJS, GRID>(sc, a, item, lane, acc[wave], accum, out, nseg, cam_lds);
   add_segments(nseg, lane, segments);
 }
 
@@ -272,14 +318,16 @@ __global__ __launch_bounds__(64 * kPWaves) void render_persistent(View sc, Args 
   __shared__ unsigned long long acc[kPWaves][3][64];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  stage_scene<true, LDS_OBJS, GRID>(sc);
+  __shared__ float cam_lds[23];
+  stage_camera(cam_lds, a);
+  stage_scene<true, LDS_OBJS, GRID>(sc);  // (its barrier covers the camera)
   unsigned nseg = 0;
   for (;;) {  // every wave leaves when the counter passes n_items
     unsigned it = 0;
     if (lane == 0) it = atomicAdd(counter, 1u);
     it = __builtin_amdgcn_readfirstlane(__shfl(it, 0));
     if (int(it) >= a.n_items) break;
-    run_item<CHUNKED, true, LDS_OBJS, GRID>(sc, a, int(it), lane, acc[wave], accum, out, nseg);
+    run_item<CHUNKED, true, LDS_OBJS, GRID>(sc, a, int(it), lane, acc[wave], accum, out, nseg, cam_lds);
   }
   add_segments(nseg, lane, segments);
 }

@@ -1439,6 +1439,18 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
     g[k] = make_float4(cx, cy, cz, S);
     s0[k] = make_float4(1.0f / r, float(m[0]), float(m[1]), float(m[2]));
     s1[k] = make_float4(float(kind), float(fuzz), ir, 1.0f / ir);
+    if (kind == RT_MAT_DIELECTRIC) {
+      // Schlick's r0 for both faces (material.h:91-96), in the float
+      // arithmetic the kernels would repeat per scatter: front (ratio 1/ir)
+      // in shade1.y, back (ratio ir) in shade0.y — fields a dielectric does
+      // not otherwise read (no albedo, no fuzz)
+      auto r0_of = [](float x) {
+        const float q = (1.0f - x) / (1.0f + x);
+        return q * q;
+      };
+      s1[k].y = r0_of(1.0f / ir);
+      s0[k].y = r0_of(ir);
+    }
     g64[k] = make_double4(c[0], c[1], c[2], c[3] * c[3]);
     s064[k] = make_double4(1 / c[3], m[0], m[1], m[2]);
     s164[k] = make_double4(double(kind), fuzz, m[3], 1.0 / m[3]);

@@ -1179,7 +1179,10 @@ __device__ __forceinline__ bool scatter_fast(const float4 s0, const float4 s1, V
   const float sin_theta = dsqrt(__builtin_fmaf(-cos_theta, cos_theta, 1.0f));
   const bool cannot_refract = ratio * sin_theta > 1.0f;
   if (cannot_refract) g = g0;  // the uniform is not drawn
-  if (cannot_refract || reflectance<true>(cos_theta, ratio) > u)
+  // Schlick with r0 precomputed per face by the host (rt_ctx_set_scene):
+  // reflectance<true>(cos_theta, ratio) without its division
+  const float r0 = front ? s1.y : s0.y;
+  if (cannot_refract || __builtin_fmaf(1.0f - r0, pow5(1.0f - cos_theta), r0) > u)
     dout = refl;
   else
     dout = refract<true>(ud, normal, ratio, cos_theta);

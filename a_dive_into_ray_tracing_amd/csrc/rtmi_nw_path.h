@@ -230,6 +230,46 @@ __device__ __forceinline__ int hit_box(V o, V d, const float4 p0, const float4 p
   return face;
 }
 
+// The rectangles and boxes of hit_object (objects; media boundaries keep the
+// division forms above): the plane parameter as (k - o_k) * inv_d_k with
+// inv_d = 1/d per axis — of the world ray, computed once per segment, or of
+// an instanced object's local ray — instead of a division per plane (six per
+// box test).  The oracle's nw_hit_*_inv are the same expressions.
+template <int KA, int AA, int BA>
+__device__ __forceinline__ bool hit_rect_inv(V o, V d, V inv, float a0, float a1, float b0, float b1, float k,
+                                             float tmin, float tmax, float &t) {
+  const float ok = KA == 0 ? o.x : KA == 1 ? o.y : o.z;
+  const float ik = KA == 0 ? inv.x : KA == 1 ? inv.y : inv.z;
+  const float tt = (k - ok) * ik;
+  if (tt < tmin || tt > tmax) return false;
+  const float oa = AA == 0 ? o.x : o.y, da = AA == 0 ? d.x : d.y;
+  const float ob = BA == 1 ? o.y : o.z, db = BA == 1 ? d.y : d.z;
+  const float x = __builtin_fmaf(tt, da, oa);
+  const float y = __builtin_fmaf(tt, db, ob);
+  if (x < a0 || x > a1 || y < b0 || y > b1) return false;
+  t = tt;
+  return true;
+}
+__device__ __forceinline__ bool hit_rect_kind_inv(int kind, V o, V d, V inv, const float4 g, float k, float tmin,
+                                                  float tmax, float &t) {
+  if (kind == kRectXY) return hit_rect_inv<2, 0, 1>(o, d, inv, g.x, g.y, g.z, g.w, k, tmin, tmax, t);
+  if (kind == kRectXZ) return hit_rect_inv<1, 0, 2>(o, d, inv, g.x, g.y, g.z, g.w, k, tmin, tmax, t);
+  return hit_rect_inv<0, 1, 2>(o, d, inv, g.x, g.y, g.z, g.w, k, tmin, tmax, t);
+}
+__device__ __forceinline__ int hit_box_inv(V o, V d, V inv, const float4 p0, const float4 p1, float tmin, float tmax,
+                                           float &t) {
+  int face = -1;
+  float closest = tmax, tt;
+  if (hit_rect_inv<2, 0, 1>(o, d, inv, p0.x, p1.x, p0.y, p1.y, p1.z, tmin, closest, tt)) { closest = tt; face = 0; }
+  if (hit_rect_inv<2, 0, 1>(o, d, inv, p0.x, p1.x, p0.y, p1.y, p0.z, tmin, closest, tt)) { closest = tt; face = 1; }
+  if (hit_rect_inv<1, 0, 2>(o, d, inv, p0.x, p1.x, p0.z, p1.z, p1.y, tmin, closest, tt)) { closest = tt; face = 2; }
+  if (hit_rect_inv<1, 0, 2>(o, d, inv, p0.x, p1.x, p0.z, p1.z, p0.y, tmin, closest, tt)) { closest = tt; face = 3; }
+  if (hit_rect_inv<0, 1, 2>(o, d, inv, p0.y, p1.y, p0.z, p1.z, p1.x, tmin, closest, tt)) { closest = tt; face = 4; }
+  if (hit_rect_inv<0, 1, 2>(o, d, inv, p0.y, p1.y, p0.z, p1.z, p0.x, tmin, closest, tt)) { closest = tt; face = 5; }
+  t = closest;
+  return face;
+}
+
 // a medium's boundary (sphere, moving sphere or box) over (tmin, tmax)
 __device__ __forceinline__ bool hit_boundary(const Obj &ob, V o, V d, float time, float tmin, float tmax, float &t) {
   const int bk = ob.aux & 255;
@@ -273,18 +313,26 @@ __device__ __forceinline__ float medium_uniform(uint64_t seg_key, int32_t id, in
 
 // One non-medium object's hit (world ray in; t_min = 0.001, no upper bound:
 // the caller applies the order-independent closest rule).  face: box side.
-__device__ __forceinline__ bool hit_object(const View &sc, const DevObj &ob, V ow, V dw, float time, float &t,
-                                           int &face) {
+// invw = 1/dw per axis of the world ray (hit_rect_inv).
+__device__ __forceinline__ bool hit_object(const View &sc, const DevObj &ob, V ow, V dw, V invw, float time,
+                                           float &t, int &face) {
   V o = ow, d = dw;
-  if (ob.inst >= 0) to_local(sc.inst[ob.inst], o, d);
+  const bool local = ob.inst >= 0;
+  if (local) to_local(sc.inst[ob.inst], o, d);
   const float tmin = 0.001f;
   const int kind = ob.ka & 255;
   switch (kind) {
     case kSphere: return hit_sphere(o, d, mk(ob.g0[0], ob.g0[1], ob.g0[2]), ob.g0[3], tmin, INFINITY, t);
     case kMovingSphere: return hit_moving(o, d, moving_center(ob, time), ob.g0[3], tmin, INFINITY, t);
-    case kRectXY: case kRectXZ: case kRectYZ:
-      return hit_rect_kind(kind, o, d, ld4(ob.g0), ob.g1[0], tmin, INFINITY, t);
-    default: face = hit_box(o, d, ld4(ob.g0), ld4(ob.g1), tmin, INFINITY, t); return face >= 0;
+    case kRectXY: case kRectXZ: case kRectYZ: {
+      const V inv = local ? mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z) : invw;
+      return hit_rect_kind_inv(kind, o, d, inv, ld4(ob.g0), ob.g1[0], tmin, INFINITY, t);
+    }
+    default: {
+      const V inv = local ? mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z) : invw;
+      face = hit_box_inv(o, d, inv, ld4(ob.g0), ld4(ob.g1), tmin, INFINITY, t);
+      return face >= 0;
+    }
   }
 }
 
@@ -312,6 +360,7 @@ __device__ __forceinline__ int32_t hit_world_nw(const View &sc, V o, V d, float 
   int32_t best = -1, best_id = 0x7fffffff;
   best_face = -1;
   uint32_t med_hit = 0;
+  const V invw = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // hit_object's planes
   for (int32_t m = 0; m < sc.nmed; ++m) {
     const Obj ob = sc.med[m];
     const int32_t id = sc.med_id[m];
@@ -351,7 +400,7 @@ __device__ __forceinline__ int32_t hit_world_nw(const View &sc, V o, V d, float 
         const int32_t id = oids[k];
         float t;
         int face = -1;
-        if (hit_object(sc, ob, o, d, time, t, face) && (t < best_t || (t == best_t && id < best_id))) {
+        if (hit_object(sc, ob, o, d, invw, time, t, face) && (t < best_t || (t == best_t && id < best_id))) {
           best_t = t;
           best = k;
           best_id = id;
@@ -396,6 +445,7 @@ __device__ __forceinline__ int32_t hit_world_nw_grid(const View &sc, V o, V d, f
   int32_t best = -1, best_id = 0x7fffffff;
   best_face = -1;
   uint32_t med_hit = 0;
+  const V invw = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // hit_object's planes
   for (int32_t m = 0; m < sc.nmed; ++m) {
     const Obj ob = sc.med[m];
     const int32_t id = sc.med_id[m];
@@ -418,7 +468,7 @@ __device__ __forceinline__ int32_t hit_world_nw_grid(const View &sc, V o, V d, f
     const int32_t id = oids[k];
     float t;
     int face = -1;
-    if (hit_object(sc, ob, o, d, time, t, face) && (t < best_t || (t == best_t && id < best_id))) {
+    if (hit_object(sc, ob, o, d, invw, time, t, face) && (t < best_t || (t == best_t && id < best_id))) {
       best_t = t;
       best = k;
       best_id = id;

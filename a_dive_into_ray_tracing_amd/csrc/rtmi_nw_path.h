@@ -286,8 +286,35 @@ __device__ __forceinline__ float medium_uniform(uint64_t seg_key, int32_t id, in
 __device__ __forceinline__ bool hit_medium(const Obj &ob, int32_t id, V o, V d, V dw, float time, uint64_t seg_key,
                                            float &t) {
   float r1, r2;
-  if (!hit_boundary(ob, o, d, time, -INFINITY, INFINITY, r1)) return false;
-  if (!hit_boundary(ob, o, d, time, float(double(r1) + 0.00001), INFINITY, r2)) return false;
+  const int bk = ob.aux & 255;
+  if (bk == kSphere || bk == kMovingSphere) {
+    // the two boundary calls (constant_medium.h:44-48) share one quadratic:
+    // the same roots, selected as each call's interval test would
+    const bool mv = bk == kMovingSphere;
+    const V c = mv ? moving_center(ob, time) : mk(ob.g0[0], ob.g0[1], ob.g0[2]);
+    const float r = ob.g0[3];
+    const V oc = sub3(o, c);
+    const float a = dot3(d, d), b = dot3(oc, d), cc = dot3(oc, oc) - r * r;
+    const float disc = __builtin_fmaf(b, b, -(a * cc));
+    if (mv ? disc < 0.0f : !(disc > 0.0f)) return false;  // hit_moving / hit_sphere
+    const float sq = __builtin_sqrtf(disc);
+    const float q1 = (-b - sq) / a, q2 = (-b + sq) / a;
+    auto pick = [&](float tmin, float tmax, float &out) {
+      if (mv) {  // closed interval, hit_moving
+        if (!(q1 < tmin || tmax < q1)) { out = q1; return true; }
+        if (!(q2 < tmin || tmax < q2)) { out = q2; return true; }
+        return false;
+      }
+      if (q1 < tmax && q1 > tmin) { out = q1; return true; }  // open interval, hit_sphere
+      if (q2 < tmax && q2 > tmin) { out = q2; return true; }
+      return false;
+    };
+    if (!pick(-INFINITY, INFINITY, r1)) return false;
+    if (!pick(float(double(r1) + 0.00001), INFINITY, r2)) return false;
+  } else {
+    if (!hit_boundary(ob, o, d, time, -INFINITY, INFINITY, r1)) return false;
+    if (!hit_boundary(ob, o, d, time, float(double(r1) + 0.00001), INFINITY, r2)) return false;
+  }
   if (r1 < 0.0f) r1 = 0.0f;
   const float len = __builtin_sqrtf(dot3(dw, dw));
   const float inside = (r2 - r1) * len;

@@ -190,16 +190,20 @@ template <bool BVH> struct GridShape {
   static constexpr int waves = BVH ? RTMI_BVH_WAVES : kWavesPerBlock;
   static constexpr int per_eu = BVH ? RTMI_ACC_PER_EU : RTMI_WAVES_PER_EU;
 };
-// Persistent-kernel block shape.  The accelerated kernels run 8-wave blocks at
-// 8 waves per SIMD (64 VGPRs): a resident grid holds its slots to the end, so
-// big blocks cost no fragmentation, and 8 waves share one staged copy of the
-// BVH/grid beside their two accumulator slots each (~35 KB: 4 blocks per CU).
+// Persistent-kernel block shape for accelerated scenes: 4-wave blocks at 6
+// waves per SIMD (79 VGPRs, no spills; two accumulator slots per wave beside
+// the staged grid, ~23 KB per block).  Config 2 frame / 1/8 strip, grid:
+// 8-wave blocks at 8 waves/SIMD (17 VGPRs spilled) 33.2 / 5.01 ms, 4-wave at
+// 7 waves/SIMD 33.2 / 5.01, 4-wave at 6: 30.9 / 4.72 (profiles/r02/ab_persistent/).
 #ifndef RTMI_PERSIST_ACC_WAVES
-#define RTMI_PERSIST_ACC_WAVES 8
+#define RTMI_PERSIST_ACC_WAVES 4
+#endif
+#ifndef RTMI_PERSIST_ACC_PER_EU
+#define RTMI_PERSIST_ACC_PER_EU 6
 #endif
 template <int ACC> struct PersistShape {
   static constexpr int waves = ACC ? RTMI_PERSIST_ACC_WAVES : kWavesPerBlock;
-  static constexpr int per_eu = ACC ? RTMI_ACC_PER_EU : RTMI_PERSIST_MIN_BLOCKS;
+  static constexpr int per_eu = ACC ? RTMI_PERSIST_ACC_PER_EU : RTMI_PERSIST_MIN_BLOCKS;
 };
 
 #if RTMI_CAM_LDS

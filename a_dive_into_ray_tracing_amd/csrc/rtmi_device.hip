@@ -1733,7 +1733,14 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   const bool persistent = ctx->kernel == RT_KERNEL_PERSISTENT ||
                           (ctx->kernel == RT_KERNEL_AUTO && !bvh && tile_samples < 6000000);
   int32_t chunk1 = ctx->chunk, chunk2 = ctx->tail_chunk, tail = ctx->tail_spp;
-  if (chunk1 <= 0 && persistent) {
+  if (chunk1 <= 0 && persistent && bvh) {
+    // accelerated scenes: ~8 items per resident wave, 8..32 samples (grid,
+    // 1/8 strip: chunk 8 -> 4.41 ms, 16 -> 4.27, 32 -> 4.43, 64 -> 6.69; frame
+    // 31.0-32.9 for 8..64; profiles/r02/ab_persistent/pers_chunk)
+    const int64_t waves = int64_t(acc_kind == 1 ? ctx->resident_blocks_bvh : ctx->resident_blocks_grid) *
+                          (acc_kind == 1 ? PersistShape<1>::waves : PersistShape<2>::waves);
+    chunk1 = int32_t(std::min<int64_t>(32, std::max<int64_t>(8, tile_samples / (8 * waves))));
+  } else if (chunk1 <= 0 && persistent) {
     // ~28 items per resident wave (1/8 strip: chunk 8 -> 17.5 ms, 16 -> 17.9, 32 -> 19.7)
     const int64_t waves = int64_t(ctx->resident_blocks) * kWavesPerBlock;
     chunk1 = int32_t(std::min<int64_t>(64, std::max<int64_t>(4, tile_samples / (28 * waves))));

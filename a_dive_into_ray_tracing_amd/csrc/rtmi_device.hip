@@ -132,6 +132,13 @@ __device__ unsigned g_trace_n;
 #ifndef RTMI_CAM_LDS
 #define RTMI_CAM_LDS 1
 #endif
+// Fast mode: u, v = (i + ju) * (1/(W-1)), (j + jv) * (1/(H-1)) — the
+// reciprocals once per block instead of two divisions per camera ray (<= 1
+// ulp from main.cpp:278-279's quotients; the oracle's fast mode computes the
+// same products).  0: the quotients (A/B only; the oracle does not follow).
+#ifndef RTMI_UV_RCP
+#define RTMI_UV_RCP 1
+#endif
 #ifndef RTMI_REGEN_TWICE
 #define RTMI_REGEN_TWICE 0
 #endif
@@ -224,7 +231,11 @@ __device__ __forceinline__ void stage_camera(float *cam_lds, const RenderArgs &a
     }
     cam_lds[t] = v;
   } else if (t < 21) {
+#if RTMI_UV_RCP
+    cam_lds[t] = 1.0f / float((t == 19 ? a.W : a.H) - 1);
+#else
     cam_lds[t] = float((t == 19 ? a.W : a.H) - 1);
+#endif
   }
 }
 __device__ __forceinline__ Cam<float> lds_camera(const float *cam_lds) {
@@ -254,7 +265,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
 #if RTMI_CAM_LDS
   // the camera in LDS, read at each regeneration: kept out of the wave's
   // scalar registers (which spill it to VGPR lanes otherwise)
-  __shared__ float cam_lds[20];
+  __shared__ float cam_lds[21];
 #endif
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -275,6 +286,9 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
     }
     cam_lds[threadIdx.x] = v;
   }
+#if RTMI_UV_RCP
+  else if (threadIdx.x < 21) cam_lds[threadIdx.x] = 1.0f / float((threadIdx.x == 19 ? a.W : a.H) - 1);
+#endif
   if constexpr (ACC == 0) __syncthreads();  // (accelerated kernels: stage_* ends with one)
 #endif
   if constexpr (ACC == 1) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
@@ -346,8 +360,14 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
     rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(a.s_base + s));
     float ju, jv;
     rng.pair(ju, jv);
+#if RTMI_UV_RCP
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const float u = (float(i) + ju) * cam_lds[19];  // main.cpp:278, by the reciprocal
+    const float v = (float(j) + jv) * cam_lds[20];  // main.cpp:279
+#else
     const float u = (float(i) + ju) / float(a.W - 1);  // main.cpp:278
     const float v = (float(j) + jv) / float(a.H - 1);  // main.cpp:279
+#endif
 #if RTMI_CAM_LDS
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // read here, not hoisted out of the loop
     Cam<float> cm;
@@ -702,8 +722,13 @@ __global__ __launch_bounds__(64 * PersistShape<ACC>::waves, PersistShape<ACC>::p
           float ju, jv;
           rng.pair(ju, jv);
 #if RTMI_CAM_LDS
+#if RTMI_UV_RCP
+          const float u = (float(i) + ju) * cam_lds[19];  // main.cpp:278, by the reciprocal
+          const float v = (float(j) + jv) * cam_lds[20];  // main.cpp:279
+#else
           const float u = (float(i) + ju) / cam_lds[19];  // main.cpp:278
           const float v = (float(j) + jv) / cam_lds[20];  // main.cpp:279
+#endif
           get_ray<true, float>(lds_camera(cam_lds), u, v, rng, o, d);
 #else
           const float u = (float(i) + ju) / float(a.W - 1);  // main.cpp:278

@@ -31,8 +31,12 @@
 #ifndef RTMI_GRID_DIRECT
 #define RTMI_GRID_DIRECT 0
 #endif
+// Fast-mode seeding: s0 = mix64(seed ^ key*phi), s1 = mix64(s0 + phi) — the
+// splitmix64 construction with the (pixel, sample) key as its counter; one
+// 64-bit multiply instead of a third mix64 (the oracle's xo_init is the same;
+// 0 selects the round-1 three-mix64 seeding, for A/B only)
 #ifndef RTMI_CHEAP_SEED
-#define RTMI_CHEAP_SEED 0
+#define RTMI_CHEAP_SEED 1
 #endif
 
 namespace rtmi {

@@ -70,7 +70,7 @@ static inline uint64_t mix64(uint64_t z) {
 }
 static inline void xo_init(xo *g, uint64_t seed, uint64_t pixel, uint32_t sample) {
   uint64_t key = (pixel << 24) | (uint64_t)sample;
-  g->s0 = mix64(seed ^ mix64(key + 0x9E3779B97F4A7C15ULL));
+  g->s0 = mix64(seed ^ (key * 0x9E3779B97F4A7C15ULL)); /* splitmix64 with the key as counter */
   g->s1 = mix64(g->s0 + 0x9E3779B97F4A7C15ULL);
 }
 static inline uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }

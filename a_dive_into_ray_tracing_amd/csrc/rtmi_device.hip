@@ -1830,7 +1830,6 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
       if (rc) { ctx->accum_cap = 0; return rc; }
       ctx->accum_cap = n_valid_out;
     }
-    HIP_TRY(hipMemsetAsync(ctx->accum, 0, n_valid_out * sizeof(unsigned long long), st));
   }
   // (after the allocation above, which may replace ctx->accum)
   unsigned long long *const accum = pass_accum ? pass_accum : ctx->accum;
@@ -1898,6 +1897,10 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     std::copy(key, key + 6, ctx->cost_key);
     ctx->cost_valid = true;
   }
+  // (cleared here, after the cost probe, which may render into the same
+  // accumulator)
+  if (chunked && !pass_accum && !a.block_owns_tile)
+    HIP_TRY(hipMemsetAsync(ctx->accum, 0, n_valid_out * sizeof(unsigned long long), st));
   dim3 grid;
   if (persistent) {
     // a resident grid of waves pulling items from a global counter

@@ -544,6 +544,27 @@ def main():
                 "walk_lane_utilisation": round(counts["node_visits"] / max(1, 64 * counts["node_iterations_wave"]), 4),
                 "leaf_lane_utilisation": round(counts["leaf_sphere_tests"] / max(1, 64 * counts["leaf_sphere_iterations_wave"]), 4),
             }
+        # Context beside the algorithmic fraction, from the committed PMC passes
+        # of the same kernel on the same workload (tools/profile.sh,
+        # profiles/pmc_valu.json) over this run's kernel time: every FP32 FLOP
+        # the kernel executes (shading, regeneration and idle-lane slots
+        # included) and how busy the VALU issue is — the bound of this
+        # divergent kernel
+        pmcv = os.path.join(REPO, "profiles", "pmc_valu.json")
+        if os.path.exists(pmcv) and args.workload == "config2" and args.accel == "grid" and not args.strip_of and N == 1:
+            try:
+                pv = json.load(open(pmcv))
+                ks = kernel_ms * 1e-3
+                roof["pmc"] = {
+                    "source": "profiles/pmc_valu.json",
+                    "executed_fp32_flop_per_launch": pv["executed_fp32_flop_per_launch"],
+                    "executed_fp32_frac": round(pv["executed_fp32_flop_per_launch"] / ks / 1e12 / PEAK_FP32_TFLOPS, 4),
+                    "valu_issue_busy": round(pv["per_launch"]["SQ_INSTS_VALU"] * 2 / (1024 * 2.4e9 * ks), 4),
+                    "lane_utilisation": round(pv["lane_utilisation"], 4),
+                    "wait_fraction": round(pv["wait_fraction"], 4),
+                }
+            except Exception:
+                pass
         if why:
             roof["note"] = why
         line = {

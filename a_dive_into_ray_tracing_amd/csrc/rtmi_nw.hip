@@ -60,6 +60,19 @@ struct Args {
 constexpr int kWaves = RTMI_NW_WAVES;                         // grid kernel: waves per block
 constexpr size_t kLdsBudget = size_t(RTMI_NW_LDS_KB) * 1024;  // grid kernel: staged bytes per block
 constexpr int kPWaves = 16;                                   // persistent kernel: waves per block (one per CU)
+// spheres-only instantiation of the persistent kernel: waves per block and
+// the minimum waves per SIMD it is compiled for (VGPR budget 512 / per_eu).
+// Motion-blur scene 1200x800x500 (profiles/r02/ab_nw_spheres_only/): general
+// kernel 100.6 ms; spheres-only at 89 VGPRs (4 waves per SIMD) 79.2;
+// 8-wave blocks at 6 per SIMD (80 VGPRs, 7 spilled) 63.8; 16- or 8-wave
+// blocks at 8 per SIMD (64 VGPRs, spills) 60.4-60.5
+#ifndef RTMI_NW_SIMPLE_WAVES
+#define RTMI_NW_SIMPLE_WAVES 16
+#endif
+#ifndef RTMI_NW_SIMPLE_PER_EU
+#define RTMI_NW_SIMPLE_PER_EU 8
+#endif
+template <bool S> constexpr int persist_waves() { return S ? RTMI_NW_SIMPLE_WAVES : kPWaves; }
 constexpr size_t kPLdsBudget = 136 * 1024;                    // persistent kernel: staged bytes (+ 24 KB accumulators)
 
 // RTMI_NW_PHASES builds (analysis only): wave-level cycles (s_memtime) of a
@@ -138,7 +151,7 @@ __device__ __forceinline__ void stage_scene(const View &sc) {
 // One work item = (8x8 tile, <= chunk samples) on one wave: lanes pull
 // (pixel, sample) jobs from the item's queue and regenerate paths as theirs
 // end; sums in the wave's LDS accumulator, then one global add per pixel.
-template <bool CHUNKED, bool LDS_NODES, bool LDS_OBJS, bool GRID>
+template <bool CHUNKED, bool LDS_NODES, bool LDS_OBJS, bool GRID, bool S = false>
 __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item, int lane,
                                          unsigned long long (&acc)[3][64], unsigned long long *__restrict__ accum,
                                          float *__restrict__ out, unsigned &nseg, const float *cl) {
@@ -210,10 +223,10 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
 #endif
     if (active) {
       ++nseg;
-      const uint64_t seg_key = sc.has_media ? rng.next() : 0ull;
+      const uint64_t seg_key = !S && sc.has_media ? rng.next() : 0ull;
       float t;
       int face;
-      const int32_t k = GRID ? hit_world_nw_grid(sc, o, d, time, seg_key, t, face)
+      const int32_t k = GRID ? hit_world_nw_grid<S>(sc, o, d, time, seg_key, t, face)
                              : hit_world_nw<LDS_NODES, LDS_OBJS>(sc, o, d, time, seg_key, t, face);
 #if RTMI_NW_PHASES
       pb = __builtin_amdgcn_s_memtime();
@@ -222,14 +235,14 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
         col = mk(T.x * sc.bg[0], T.y * sc.bg[1], T.z * sc.bg[2]);
         done = true;
       } else {
-        const Rec rec = k < sc.nobj ? make_rec(sc, sc.obj[k], o, d, time, t, face)
-                                    : make_rec_medium(sc, sc.med[k - sc.nobj], o, d, time);
+        const Rec rec = S || k < sc.nobj ? make_rec<S>(sc, sc.obj[k], o, d, time, t, face)
+                                         : make_rec_medium(sc, sc.med[k - sc.nobj], o, d, time);
         const Mat m = sc.mat[rec.mat];
         V at, nd;
         if (m.kind == kDiffuseLight) {  // emitted, no scatter: main.cu:76-90
-          col = mul3(T, tex_value(sc, m.tex, rec.u, rec.v, rec.p));
+          col = mul3(T, tex_value<S>(sc, m.tex, rec.u, rec.v, rec.p));
           done = true;
-        } else if (!scatter_nw(sc, rec, d, rng, at, nd)) {
+        } else if (!scatter_nw<S>(sc, rec, d, rng, at, nd)) {
           done = true;  // absorbed: emitted() = 0
         } else {
           T = mul3(T, at);
@@ -309,13 +322,13 @@ __global__ __launch_bounds__(64 * kWaves) void render_kernel(View sc, Args a, un
   add_segments(nseg, lane, segments);
 }
 
-template <bool CHUNKED, bool LDS_OBJS, bool GRID>
-__global__ __launch_bounds__(64 * kPWaves) void render_persistent(View sc, Args a,
+template <bool CHUNKED, bool LDS_OBJS, bool GRID, bool S = false>
+__global__ __launch_bounds__(64 * persist_waves<S>(), S ? RTMI_NW_SIMPLE_PER_EU : 1) void render_persistent(View sc, Args a,
                                                                   unsigned long long *__restrict__ accum,
                                                                   float *__restrict__ out,
                                                                   unsigned long long *__restrict__ segments,
                                                                   unsigned *__restrict__ counter) {
-  __shared__ unsigned long long acc[kPWaves][3][64];
+  __shared__ unsigned long long acc[persist_waves<S>()][3][64];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   __shared__ float cam_lds[23];
@@ -327,7 +340,7 @@ __global__ __launch_bounds__(64 * kPWaves) void render_persistent(View sc, Args 
     if (lane == 0) it = atomicAdd(counter, 1u);
     it = __builtin_amdgcn_readfirstlane(__shfl(it, 0));
     if (int(it) >= a.n_items) break;
-    run_item<CHUNKED, true, LDS_OBJS, GRID>(sc, a, int(it), lane, acc[wave], accum, out, nseg, cam_lds);
+    run_item<CHUNKED, true, LDS_OBJS, GRID, S>(sc, a, int(it), lane, acc[wave], accum, out, nseg, cam_lds);
   }
   add_segments(nseg, lane, segments);
 }
@@ -424,6 +437,14 @@ struct rt_nw_ctx {
   unsigned long long *segments = nullptr;
   unsigned *counter = nullptr;  // persistent kernel's work-item counter
   int32_t persist_blocks = 0;   // resident 16-wave blocks (CUs x blocks per CU)
+  // spheres-only scene (spheres and moving spheres, no instances or media,
+  // solid and checker-of-solid textures): the persistent grid kernel's S
+  // instantiation, with the other kinds' code compiled out (fewer VGPRs, more
+  // waves); RTMI_NW_SIMPLE=0 turns it off (A/B and tests)
+  bool simple = false;
+  bool simple_ok = !(std::getenv("RTMI_NW_SIMPLE") && std::getenv("RTMI_NW_SIMPLE")[0] == '0');
+  int32_t persist_blocks_simple = 0;
+  int32_t last_kernel[4] = {0, 0, 0, 0};  // rt_nw_ctx_last_kernel
   // samples per work item forced by RTMI_NW_CHUNK (A/B only; 0 = automatic),
   // read when the context is created
   int32_t env_chunk = std::getenv("RTMI_NW_CHUNK") ? std::atoi(std::getenv("RTMI_NW_CHUNK")) : 0;
@@ -516,6 +537,10 @@ RTMI_EXPORT int rt_nw_ctx_create(int32_t device, rt_nw_ctx **out) {
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<true, false, false>,
                                                          64 * kPWaves, 0));
     ctx->persist_blocks = per_cu * prop.multiProcessorCount;
+    per_cu = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<true, true, true, true>,
+                                                         64 * persist_waves<true>(), 0));
+    ctx->persist_blocks_simple = per_cu * prop.multiProcessorCount;
   }
   *out = ctx.release();
   return RT_OK;
@@ -637,6 +662,12 @@ RTMI_EXPORT int rt_nw_ctx_set_scene(rt_nw_ctx *ctx, rt_nw_scene *s) {
   ctx->ntex = nt;
   for (int c = 0; c < 3; ++c) ctx->bg[c] = ds.background[c];
   ctx->has_media = ds.has_media ? 1 : 0;
+  bool simple = ds.med.empty();
+  for (const Obj &o : ds.obj) simple = simple && o.inst < 0 && (o.kind == kSphere || o.kind == kMovingSphere);
+  for (const Tex &t : ds.tex)
+    simple = simple && (t.kind == kSolid || (t.kind == kChecker && ds.tex[size_t(t.a)].kind == kSolid &&
+                                             ds.tex[size_t(t.b)].kind == kSolid));
+  ctx->simple = simple;
   return RT_OK;
 }
 
@@ -713,6 +744,10 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
   const size_t gbytes = use_grid ? grid_bytes(ctx) : 0;
   const bool persist = RTMI_NW_PERSIST && ctx->persist_blocks > 0 &&
                        (use_grid || (ctx->nnodes > 0 && node_bytes <= kPLdsBudget));
+  // the spheres-only instantiation of the persistent grid kernel
+  const bool simple = persist && use_grid && ctx->simple && ctx->simple_ok && ctx->persist_blocks_simple > 0;
+  const int32_t pblocks = simple ? ctx->persist_blocks_simple : ctx->persist_blocks;
+  const int64_t pwaves = simple ? persist_waves<true>() : kPWaves;
   // samples per work item (same image for any size; RTMI_NW_CHUNK overrides,
   // for A/B).  Persistent kernel: ~80 items per resident wave, 4..32 samples:
   // the final scene (fog, lights: long and uneven paths) at 256 spp runs 329
@@ -721,7 +756,7 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
   // (profiles/r01/session6/nw_chunk.txt).  Grid kernel: 32.
   int64_t chunk = 32;
   if (persist) {
-    const int64_t waves = int64_t(ctx->persist_blocks) * kPWaves;
+    const int64_t waves = int64_t(pblocks) * pwaves;
     chunk = std::min<int64_t>(32, std::max<int64_t>(4, int64_t(a.tiles) * spp / (80 * waves)));
   }
   a.chunk = std::min<int64_t>(spp, ctx->env_chunk > 0 ? ctx->env_chunk : chunk);
@@ -749,12 +784,18 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
   const size_t lds = use_grid ? gbytes
                      : persist ? (p_objs ? node_bytes + obj_bytes : node_bytes)
                                : lds_objs ? node_bytes + obj_bytes : lds_nodes ? node_bytes : 0;
-  const unsigned blocks = persist ? unsigned(std::min<int64_t>(ctx->persist_blocks, (a.n_items + kPWaves - 1) / kPWaves))
+  const unsigned blocks = persist ? unsigned(std::min<int64_t>(pblocks, (a.n_items + pwaves - 1) / pwaves))
                                   : unsigned((a.n_items + kWaves - 1) / kWaves);
   if (persist) HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
+  ctx->last_kernel[0] = persist ? 1 : 0;
+  ctx->last_kernel[1] = use_grid ? 1 : 0;
+  ctx->last_kernel[2] = simple ? 1 : 0;
+  ctx->last_kernel[3] = a.chunk;
   auto launch = [&](auto chunked) {
     constexpr bool C = decltype(chunked)::value;
-    if (persist && use_grid)
+    if (simple)
+      hipLaunchKernelGGL((render_persistent<C, true, true, true>), dim3(blocks), dim3(64 * persist_waves<true>()), lds, st, v, a, ctx->accum, dev_strip, ctx->segments, ctx->counter);
+    else if (persist && use_grid)
       hipLaunchKernelGGL((render_persistent<C, true, true>), dim3(blocks), dim3(64 * kPWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments, ctx->counter);
     else if (persist && p_objs)
       hipLaunchKernelGGL((render_persistent<C, true, false>), dim3(blocks), dim3(64 * kPWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments, ctx->counter);
@@ -847,6 +888,12 @@ RTMI_EXPORT int rt_nw_debug_phases(uint64_t *out4) {
   (void)out4;
   return set_error(RT_EUNSUPPORTED, "rt_nw_debug_phases: not an RTMI_NW_PHASES build");
 #endif
+}
+
+RTMI_EXPORT int rt_nw_ctx_last_kernel(rt_nw_ctx *ctx, int32_t *out4) {
+  if (!ctx || !out4) return set_error(RT_EINVAL, "null");
+  for (int q = 0; q < 4; ++q) out4[q] = ctx->last_kernel[q];
+  return RT_OK;
 }
 
 RTMI_EXPORT int rt_nw_ctx_last_segments(rt_nw_ctx *ctx, uint64_t *segments) {

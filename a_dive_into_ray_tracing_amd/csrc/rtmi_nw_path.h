@@ -341,8 +341,16 @@ __device__ __forceinline__ float medium_uniform(uint64_t seg_key, int32_t id, in
 // One non-medium object's hit (world ray in; t_min = 0.001, no upper bound:
 // the caller applies the order-independent closest rule).  face: box side.
 // invw = 1/dw per axis of the world ray (hit_rect_inv).
+// S: a spheres-only scene (rt_nw_ctx_set_scene's check: spheres and moving
+// spheres, no instances, no media, solid and checker textures): the other
+// kinds' code is compiled out — the same arithmetic for the kinds that remain.
+template <bool S = false>
 __device__ __forceinline__ bool hit_object(const View &sc, const DevObj &ob, V ow, V dw, V invw, float time,
                                            float &t, int &face) {
+  if constexpr (S) {
+    if ((ob.ka & 255) == kSphere) return hit_sphere(ow, dw, mk(ob.g0[0], ob.g0[1], ob.g0[2]), ob.g0[3], 0.001f, INFINITY, t);
+    return hit_moving(ow, dw, moving_center(ob, time), ob.g0[3], 0.001f, INFINITY, t);
+  }
   V o = ow, d = dw;
   const bool local = ob.inst >= 0;
   if (local) to_local(sc.inst[ob.inst], o, d);
@@ -459,6 +467,7 @@ __host__ __device__ constexpr size_t nw_grid_lds_bytes(int32_t nobj, int32_t nce
 // its coordinate scale), so inside a cell that lists it; an object listed in
 // several cells gives the same t each time.  The objects' boxes cover the
 // whole shutter (moving spheres) and the composed transform (instances).
+template <bool S = false>
 __device__ __forceinline__ int32_t hit_world_nw_grid(const View &sc, V o, V d, float time, uint64_t seg_key,
                                                      float &best_t, int &best_face) {
   const DevObj *objs = reinterpret_cast<const DevObj *>(nw_nodes_lds);
@@ -472,30 +481,33 @@ __device__ __forceinline__ int32_t hit_world_nw_grid(const View &sc, V o, V d, f
   int32_t best = -1, best_id = 0x7fffffff;
   best_face = -1;
   uint32_t med_hit = 0;
-  const V invw = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // hit_object's planes
-  for (int32_t m = 0; m < sc.nmed; ++m) {
-    const Obj ob = sc.med[m];
-    const int32_t id = sc.med_id[m];
-    V lo = o, ld = d;
-    if (ob.inst >= 0) to_local(sc.inst[ob.inst], lo, ld);
-    float t;
-    if (hit_medium(ob, id, lo, ld, d, time, seg_key, t) && !(t < 0.001f)) {
-      med_hit |= 1u << m;
-      if (t < best_t || (t == best_t && id < best_id)) {
-        best_t = t;
-        best = sc.nobj + m;
-        best_id = id;
+  V invw = mk(0.f, 0.f, 0.f);
+  if constexpr (!S) {
+    invw = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // hit_object's planes
+    for (int32_t m = 0; m < sc.nmed; ++m) {
+      const Obj ob = sc.med[m];
+      const int32_t id = sc.med_id[m];
+      V lo = o, ld = d;
+      if (ob.inst >= 0) to_local(sc.inst[ob.inst], lo, ld);
+      float t;
+      if (hit_medium(ob, id, lo, ld, d, time, seg_key, t) && !(t < 0.001f)) {
+        med_hit |= 1u << m;
+        if (t < best_t || (t == best_t && id < best_id)) {
+          best_t = t;
+          best = sc.nobj + m;
+          best_id = id;
+        }
       }
     }
   }
   auto test = [&](int32_t k) {
     const DevObj ob = objs[k];
     const int twin = ob.ka >> 8;
-    if (twin > 0 && ((med_hit >> (twin - 1)) & 1u)) return;  // hidden by its medium
+    if (!S && twin > 0 && ((med_hit >> (twin - 1)) & 1u)) return;  // hidden by its medium
     const int32_t id = oids[k];
     float t;
     int face = -1;
-    if (hit_object(sc, ob, o, d, invw, time, t, face) && (t < best_t || (t == best_t && id < best_id))) {
+    if (hit_object<S>(sc, ob, o, d, invw, time, t, face) && (t < best_t || (t == best_t && id < best_id))) {
       best_t = t;
       best = k;
       best_id = id;
@@ -613,12 +625,14 @@ __device__ __forceinline__ V tex_leaf(const View &sc, const Tex &tx, float u, fl
 }
 // texture value; checker_texture::value texture.h:48-55 selects by the sign
 // of sin(10x) sin(10y) sin(10z)
+template <bool S = false>
 __device__ __forceinline__ V tex_value(const View &sc, int32_t tid, float u, float v, V p) {
   Tex tx = sc.tex[tid];
   if (tx.kind == kChecker) {
     const float sines = (nw_sinf(10.0f * p.x) * nw_sinf(10.0f * p.y)) * nw_sinf(10.0f * p.z);
     tx = sc.tex[sines < 0.0f ? tx.b : tx.a];
   }
+  if constexpr (S) return mk(tx.rgb[0], tx.rgb[1], tx.rgb[2]);  // (solid leaves only)
   return tex_leaf(sc, tx, u, v, p);
 }
 __device__ __forceinline__ bool tex_needs_uv(const View &sc, int32_t tid) {
@@ -659,11 +673,20 @@ __device__ __forceinline__ Rec make_rec_medium(const View &sc, const Obj &ob, V 
   r.n = mk(1.0f, 0.0f, 0.0f);
   return r;
 }
+template <bool S = false>
 __device__ __forceinline__ Rec make_rec(const View &sc, const DevObj &ob, V ow, V dw, float time, float t, int face) {
   Rec r;
   r.mat = ob.mat;
   r.u = 0.0f;
   r.v = 0.0f;
+  if constexpr (S) {  // a sphere, no instance, no texture reads u, v
+    const V c = (ob.ka & 255) == kSphere ? mk(ob.g0[0], ob.g0[1], ob.g0[2]) : moving_center(ob, time);
+    const float inv_r = 1.0f / ob.g0[3];
+    const V p = at3(ow, dw, t);
+    r.n = mk(inv_r * (p.x - c.x), inv_r * (p.y - c.y), inv_r * (p.z - c.z));
+    r.p = p;
+    return r;
+  }
   V o = ow, d = dw;
   Inst in{1.f, 0.f, {0.f, 0.f, 0.f}, 0, {0, 0}};
   if (ob.inst >= 0) {
@@ -720,6 +743,7 @@ __device__ __forceinline__ float schlick(float cosine, float ri) {
 }
 // Returns true if the ray scattered (dir, atten set); emitted light is
 // handled by the caller.
+template <bool S = false>
 __device__ __forceinline__ bool scatter_nw(const View &sc, const Rec &rec, V din, Xoro &g, V &atten, V &dir) {
   const Mat m = sc.mat[rec.mat];
   switch (m.kind) {
@@ -727,7 +751,7 @@ __device__ __forceinline__ bool scatter_nw(const View &sc, const Rec &rec, V din
       const V rs = in_sphere_direct(g);
       const V target = add3(add3(rec.p, rec.n), rs);
       dir = sub3(target, rec.p);
-      atten = tex_value(sc, m.tex, rec.u, rec.v, rec.p);
+      atten = tex_value<S>(sc, m.tex, rec.u, rec.v, rec.p);
       return true;
     }
     case kMetal: {  // material.h:72-86
@@ -735,7 +759,7 @@ __device__ __forceinline__ bool scatter_nw(const View &sc, const Rec &rec, V din
       const V rs = in_sphere_direct(g);
       dir = mk(__builtin_fmaf(m.fuzz, rs.x, refl.x), __builtin_fmaf(m.fuzz, rs.y, refl.y),
                __builtin_fmaf(m.fuzz, rs.z, refl.z));
-      atten = tex_value(sc, m.tex, rec.u, rec.v, rec.p);
+      atten = tex_value<S>(sc, m.tex, rec.u, rec.v, rec.p);
       return dot3(dir, rec.n) > 0.0f;
     }
     case kDielectric: {  // material.h:119-148 (+ refract :103-114)
@@ -773,7 +797,7 @@ __device__ __forceinline__ bool scatter_nw(const View &sc, const Rec &rec, V din
     }
     case kIsotropic: {  // material.h:180-190
       dir = in_sphere_direct(g);
-      atten = tex_value(sc, m.tex, rec.u, rec.v, rec.p);
+      atten = tex_value<S>(sc, m.tex, rec.u, rec.v, rec.p);
       return true;
     }
     default: return false;  // diffuse_light material.h:159-177

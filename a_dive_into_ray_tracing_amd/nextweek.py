@@ -255,6 +255,12 @@ class NwRenderer:
         check(load().rt_nw_ctx_last_segments(self._h, C.byref(v)), "rt_nw_ctx_last_segments")
         return v.value
 
+    def last_kernel(self):
+        """Diagnostic: the last render's kernel (rt_nw_ctx_last_kernel)."""
+        v = (C.c_int32 * 4)()
+        check(load().rt_nw_ctx_last_kernel(self._h, v), "rt_nw_ctx_last_kernel")
+        return dict(zip(("persistent", "grid", "spheres_only", "chunk"), list(v)))
+
     def close(self):
         if self._h:
             load().rt_nw_ctx_destroy(self._h)

@@ -175,6 +175,11 @@ int rt_nw_debug_trace(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32_t W, int32_
                       uint64_t seed, int32_t i, int32_t j, int32_t s, float *rec, int32_t cap, int32_t *n);
 /* world.hit calls of the last render (waits for it). */
 int rt_nw_ctx_last_segments(rt_nw_ctx *ctx, uint64_t *segments);
+/* Diagnostic: the kernel of the last render, {persistent, uniform grid,
+ * spheres-only instantiation (spheres and moving spheres, no instances or
+ * media, solid / checker textures: the other kinds' code compiled out),
+ * samples per work item}.  Same image for every choice. */
+int rt_nw_ctx_last_kernel(rt_nw_ctx *ctx, int32_t *out4);
 /* Analysis builds only (-DRTMI_NW_PHASES=1): wave-level cycles of the loop
  * passes since the last call — closest hit, hit record + texture + scatter,
  * accumulation + regeneration, whole items; RT_EUNSUPPORTED otherwise. */

@@ -583,3 +583,31 @@ def test_default_accel_is_grid(final_world):
         assert r.last_schedule()["bvh"] == 2
     finally:
         r.close()
+
+
+@pytest.mark.parametrize("G", [2, 3, 4, 8])
+def test_config3_strips_unpermute_to_config2_frame(G, config2, final_world):
+    """BASELINE config 3's partition on one GPU: every rank's interleaved
+    strip of config 2 (rank g renders rows g, g+G, ...; dist.strip_rows),
+    rendered through the default (grid) path and un-permuted as rank 0 does
+    after the gather (dist.unpermute), equals the one-GPU frame bit for bit —
+    G = 3 leaves a ragged last strip (800 = 3 x 267 - 1)."""
+    torch = pytest.importorskip("torch")
+    from a_dive_into_ray_tracing_amd import dist as rdist
+
+    cam, img = config2
+    W, H, S = 1200, 800, 500
+    r = rt.Renderer(final_world, 0)
+    strips = []
+    try:
+        for g in range(G):
+            row0, step, nrows = rdist.strip_rows(H, g, G)
+            s = torch.full((nrows, W, 3), -1.0, dtype=torch.float32, device="cuda:0")
+            r.render_rows(cam, W, H, S, 50, SEED, row0, step, nrows, s.data_ptr(), 0)
+            r.synchronize()
+            assert r.last_schedule()["bvh"] == 2
+            strips.append(s.cpu().numpy())
+    finally:
+        r.close()
+    assert all(not s[-1].any() for s in strips[H % G or G:]), "rows past H must be zero-filled"
+    assert np.array_equal(rdist.unpermute(strips, H), img)

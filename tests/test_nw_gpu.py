@@ -248,3 +248,72 @@ def test_grid_mixed_objects_bit_exact(seed):
     assert np.array_equal(got, want), f"max |d| {np.abs(got - want).max()}"
     assert np.array_equal(got_bvh, want)
     assert segs == want_segs
+
+
+@pytest.mark.parametrize("which", [1, 2])
+@pytest.mark.parametrize("size", [(29, 23, 3), (64, 40, 70)])
+def test_spheres_only_kernel_bit_exact(which, size, monkeypatch, earth):
+    """Spheres-only scenes (spheres and moving spheres, solid and checker
+    textures, no instances or media) take the persistent grid kernel's
+    spheres-only instantiation (the other kinds' code compiled out); its image
+    and world.hit count equal the oracle's and the general kernel's
+    (RTMI_NW_SIMPLE=0), bit for bit.  70 spp: several items per pixel."""
+    W, H, spp = size
+    s, cam = nw.preset(which, image=earth, aspect=W / H)
+    imgs, segs = [], []
+    for simple in ("1", "0"):
+        monkeypatch.setenv("RTMI_NW_SIMPLE", simple)
+        r = nw.NwRenderer(s)
+        try:
+            r.set_accel("grid")
+            imgs.append(r.render(cam, W, H, spp, 50, SEED))
+            segs.append(r.last_segments())
+            k = r.last_kernel()
+        finally:
+            r.close()
+        assert k["persistent"] == 1 and k["grid"] == 1 and k["spheres_only"] == int(simple == "1"), k
+    want, want_segs = O.nw_render(s.flat(), cam, W, H, spp, 50, SEED)
+    assert np.array_equal(imgs[0], want), f"max |d| {np.abs(imgs[0] - want).max()}"
+    assert np.array_equal(imgs[1], want)
+    assert segs[0] == segs[1] == want_segs
+
+
+def test_spheres_only_moving_and_not_simple_scenes():
+    """Moving spheres with their own time ranges (inside and outside the
+    shutter) and a checker texture on the spheres-only kernel, bit-exact vs the
+    oracle; a scene with one rectangle, or a checker of an image texture, stays
+    on the general kernel."""
+    g = np.random.default_rng(5)
+    s = nw.Scene()
+    check = s.lambertian(s.checker(s.solid(0.2, 0.3, 0.1), s.solid(0.9, 0.9, 0.9)))
+    s.add(s.sphere((0, -1000, 0), 1000, check))
+    for k in range(120):
+        c0 = (g.uniform(-6, 6), g.uniform(0.1, 1.5), g.uniform(-6, 6))
+        c1 = (c0[0] + g.uniform(-1, 1), c0[1] + g.uniform(0, 1.2), c0[2] + g.uniform(-1, 1))
+        t0, t1 = [(0.0, 1.0), (0.2, 0.7), (-0.5, 0.5), (0.4, 2.0)][k % 4]
+        mat = [check, s.metal(s.solid(0.8, 0.7, 0.6), 0.2), s.dielectric(1.5), s.diffuse_light(s.solid(4, 4, 4))][k % 4]
+        s.add(s.moving_sphere(c0, c1, t0, t1, g.uniform(0.1, 0.4), mat) if k % 2 else
+              s.sphere(c0, g.uniform(0.1, 0.4), mat))
+    s.set_background(0.7, 0.8, 1.0)
+    W, H, spp = 40, 30, 6
+    cam = nw.camera((13, 2, 3), (0, 0, 0), (0, 1, 0), 30.0, W / H, 0.1, 10.0, 0.3, 0.6)
+    r = nw.NwRenderer(s)
+    r.set_accel("grid")
+    got, segs, k = r.render(cam, W, H, spp, 50, SEED), r.last_segments(), r.last_kernel()
+    r.close()
+    assert k["spheres_only"] == 1, k
+    want, want_segs = O.nw_render(s.flat(), cam, W, H, spp, 50, SEED)
+    assert np.array_equal(got, want), f"max |d| {np.abs(got - want).max()}"
+    assert segs == want_segs
+    for extra in ("rect", "image"):
+        s2, _ = nw.preset(2, aspect=W / H)
+        if extra == "rect":
+            s2.add(s2.rect("xy", -1, 1, -1, 1, -3, s2.lambertian(s2.solid(0.5, 0.5, 0.5))))
+        else:  # a checker with an image leaf (the missing-image texture)
+            s2.add(s2.sphere((0, 5, 0), 1, s2.lambertian(s2.checker(s2.image(None), s2.solid(1, 1, 1)))))
+        r = nw.NwRenderer(s2)
+        r.set_accel("grid")
+        r.render(cam, W, H, 2, 50, SEED)
+        k = r.last_kernel()
+        r.close()
+        assert k["spheres_only"] == 0, (extra, k)

@@ -73,6 +73,18 @@ constexpr int kPWaves = 16;                                   // persistent kern
 #define RTMI_NW_SIMPLE_PER_EU 8
 #endif
 template <bool S> constexpr int persist_waves() { return S ? RTMI_NW_SIMPLE_WAVES : kPWaves; }
+// minimum waves per SIMD of the general persistent kernel's BVH
+// instantiations: 8 (64 VGPRs, spills) lets two 16-wave blocks share a CU
+// when the staged bytes allow it.  Final scene at 1024 spp
+// (profiles/r02/ab_nw_occupancy/): nodes + objects in LDS, one block per CU
+// (100 VGPRs) 1 062 ms; objects in global memory, one block 1 185; objects
+// in global memory, two blocks at 64 VGPRs 1 009-1 013.
+#ifndef RTMI_NW_PERSIST_PER_EU
+#define RTMI_NW_PERSIST_PER_EU 8
+#endif
+// staged bytes per block (nodes, and objects when they fit) that leave room
+// for two blocks per CU beside their 24 KB accumulators (160 KB LDS per CU)
+constexpr size_t kPTwoBlockBudget = 56 * 1024;
 constexpr size_t kPLdsBudget = 136 * 1024;                    // persistent kernel: staged bytes (+ 24 KB accumulators)
 
 // RTMI_NW_PHASES builds (analysis only): wave-level cycles (s_memtime) of a
@@ -323,7 +335,7 @@ __global__ __launch_bounds__(64 * kWaves) void render_kernel(View sc, Args a, un
 }
 
 template <bool CHUNKED, bool LDS_OBJS, bool GRID, bool S = false>
-__global__ __launch_bounds__(64 * persist_waves<S>(), S ? RTMI_NW_SIMPLE_PER_EU : 1) void render_persistent(View sc, Args a,
+__global__ __launch_bounds__(64 * persist_waves<S>(), S ? RTMI_NW_SIMPLE_PER_EU : (GRID ? 1 : RTMI_NW_PERSIST_PER_EU)) void render_persistent(View sc, Args a,
                                                                   unsigned long long *__restrict__ accum,
                                                                   float *__restrict__ out,
                                                                   unsigned long long *__restrict__ segments,
@@ -436,7 +448,8 @@ struct rt_nw_ctx {
   size_t scratch_cap = 0;
   unsigned long long *segments = nullptr;
   unsigned *counter = nullptr;  // persistent kernel's work-item counter
-  int32_t persist_blocks = 0;   // resident 16-wave blocks (CUs x blocks per CU)
+  int32_t persist_blocks = 0;   // resident 16-wave blocks (CUs x blocks per CU), BVH kernels
+  int32_t persist_blocks_grid = 0;  // the same for the general grid kernel
   // spheres-only scene (spheres and moving spheres, no instances or media,
   // solid and checker-of-solid textures): the persistent grid kernel's S
   // instantiation, with the other kinds' code compiled out (fewer VGPRs, more
@@ -537,6 +550,10 @@ RTMI_EXPORT int rt_nw_ctx_create(int32_t device, rt_nw_ctx **out) {
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<true, false, false>,
                                                          64 * kPWaves, 0));
     ctx->persist_blocks = per_cu * prop.multiProcessorCount;
+    per_cu = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<true, true, true>,
+                                                         64 * kPWaves, 0));
+    ctx->persist_blocks_grid = per_cu * prop.multiProcessorCount;
     per_cu = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<true, true, true, true>,
                                                          64 * persist_waves<true>(), 0));
@@ -746,7 +763,7 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
                        (use_grid || (ctx->nnodes > 0 && node_bytes <= kPLdsBudget));
   // the spheres-only instantiation of the persistent grid kernel
   const bool simple = persist && use_grid && ctx->simple && ctx->simple_ok && ctx->persist_blocks_simple > 0;
-  const int32_t pblocks = simple ? ctx->persist_blocks_simple : ctx->persist_blocks;
+  const int32_t pblocks = simple ? ctx->persist_blocks_simple : use_grid ? ctx->persist_blocks_grid : ctx->persist_blocks;
   const int64_t pwaves = simple ? persist_waves<true>() : kPWaves;
   // samples per work item (same image for any size; RTMI_NW_CHUNK overrides,
   // for A/B).  Persistent kernel: ~80 items per resident wave, 4..32 samples:
@@ -776,7 +793,11 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
     HIP_TRY(hipMemsetAsync(dev_strip + size_t(valid) * W * 3, 0, size_t(nrows - valid) * W * 3 * sizeof(float), st));
   HIP_TRY(hipMemsetAsync(ctx->segments, 0, sizeof(unsigned long long), st));
   const View v = view_of(ctx);
-  const bool p_objs = RTMI_NW_LDS_OBJS && persist && node_bytes + obj_bytes <= kPLdsBudget;
+  // objects staged beside the nodes only when two blocks still fit a CU (or
+  // when one block per CU is all the nodes allow anyway)
+  const bool p_objs = RTMI_NW_LDS_OBJS && persist &&
+                      (node_bytes + obj_bytes <= kPTwoBlockBudget ||
+                       (node_bytes > kPTwoBlockBudget && node_bytes + obj_bytes <= kPLdsBudget));
   const bool g_grid = use_grid && !persist && gbytes <= kLdsBudget;  // grid kernel with the grid staged per block
   if (use_grid && !persist && !g_grid) return set_error(RT_EINVAL, "rt_nw: grid does not fit the grid kernel's LDS");
   const bool lds_nodes = !persist && !use_grid && ctx->nnodes > 0 && node_bytes <= kLdsBudget,

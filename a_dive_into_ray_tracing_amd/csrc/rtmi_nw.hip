@@ -334,8 +334,11 @@ __global__ __launch_bounds__(64 * kWaves) void render_kernel(View sc, Args a, un
   add_segments(nseg, lane, segments);
 }
 
+#ifndef RTMI_NW_PERSIST_GRID_PER_EU
+#define RTMI_NW_PERSIST_GRID_PER_EU 1
+#endif
 template <bool CHUNKED, bool LDS_OBJS, bool GRID, bool S = false>
-__global__ __launch_bounds__(64 * persist_waves<S>(), S ? RTMI_NW_SIMPLE_PER_EU : (GRID ? 1 : RTMI_NW_PERSIST_PER_EU)) void render_persistent(View sc, Args a,
+__global__ __launch_bounds__(64 * persist_waves<S>(), S ? RTMI_NW_SIMPLE_PER_EU : (GRID ? RTMI_NW_PERSIST_GRID_PER_EU : RTMI_NW_PERSIST_PER_EU)) void render_persistent(View sc, Args a,
                                                                   unsigned long long *__restrict__ accum,
                                                                   float *__restrict__ out,
                                                                   unsigned long long *__restrict__ segments,

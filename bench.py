@@ -345,6 +345,8 @@ def main():
                          "kernel averages must cover only the warmup + timed launches")
     ap.add_argument("--workload", choices=list(RTIOW_WORKLOADS) + ["nw_motion_blur", "nw_final"], default="config2")
     ap.add_argument("--nw-spp", type=int, default=0, help="spp of the nw_* workloads (default: 500 / 1024)")
+    ap.add_argument("--nw-preset", type=int, default=0,
+                    help="analysis only: render create_world case 1..8 at the nw_* workload's size instead")
     ap.add_argument("--nw-accel", choices=["auto", "bvh", "grid"], default="auto",
                     help="closest-hit structure of the nw_* workloads (rt_nw_ctx_set_accel; same image)")
     ap.add_argument("--strip-of", type=int, default=0,
@@ -664,6 +666,9 @@ def bench_nw(args):
         earth = None
     else:
         which, Wn, Hn, spp = 8, 800, 800, args.nw_spp or 1024
+        earth = nw.load_image(os.path.join(REPO, "tests", "golden", "earthmap.jpeg"))
+    if args.nw_preset:
+        which = args.nw_preset
         earth = nw.load_image(os.path.join(REPO, "tests", "golden", "earthmap.jpeg"))
     scene, cam = nw.preset(which, image=earth, aspect=Wn / Hn)
     r = nw.NwRenderer(scene, local_rank)

@@ -334,30 +334,6 @@ __global__ __launch_bounds__(64 * kWaves) void render_kernel(View sc, Args a, un
   add_segments(nseg, lane, segments);
 }
 
-// One wave per work item (hardware dispatch) for spheres-only scenes:
-// RTMI_NW_SG_WAVES-wave blocks at 8 waves per SIMD, the grid staged per
-// block (A/B against the persistent spheres-only kernel: RTMI_NW_SIMPLE_GRIDK)
-#ifndef RTMI_NW_SG_WAVES
-#define RTMI_NW_SG_WAVES 8
-#endif
-template <bool CHUNKED>
-__global__ __launch_bounds__(64 * RTMI_NW_SG_WAVES, 8) void render_kernel_simple(View sc, Args a,
-                                                                                 unsigned long long *__restrict__ accum,
-                                                                                 float *__restrict__ out,
-                                                                                 unsigned long long *__restrict__ segments) {
-  __shared__ unsigned long long acc[RTMI_NW_SG_WAVES][3][64];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int item = blockIdx.x * RTMI_NW_SG_WAVES + wave;
-  __shared__ float cam_lds[23];
-  stage_camera(cam_lds, a);
-  stage_scene<false, false, true>(sc);  // block barrier inside: before any wave leaves
-  if (item >= a.n_items) return;        // wave-uniform
-  unsigned nseg = 0;
-  run_item<CHUNKED, false, false, true, true>(sc, a, item, lane, acc[wave], accum, out, nseg, cam_lds);
-  add_segments(nseg, lane, segments);
-}
-
 #ifndef RTMI_NW_PERSIST_GRID_PER_EU
 #define RTMI_NW_PERSIST_GRID_PER_EU 1
 #endif
@@ -483,7 +459,6 @@ struct rt_nw_ctx {
   // waves); RTMI_NW_SIMPLE=0 turns it off (A/B and tests)
   bool simple = false;
   bool simple_ok = !(std::getenv("RTMI_NW_SIMPLE") && std::getenv("RTMI_NW_SIMPLE")[0] == '0');
-  bool simple_gridk = std::getenv("RTMI_NW_SIMPLE_GRIDK") && std::getenv("RTMI_NW_SIMPLE_GRIDK")[0] == '1';
   int32_t persist_blocks_simple = 0;
   int32_t last_kernel[4] = {0, 0, 0, 0};  // rt_nw_ctx_last_kernel
   // samples per work item forced by RTMI_NW_CHUNK (A/B only; 0 = automatic),
@@ -787,9 +762,7 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
   const size_t node_bytes = size_t(ctx->nnodes) * 32, obj_bytes = size_t(ctx->nobj) * (sizeof(DevObj) + 4);
   const bool use_grid = accel_used(ctx) == RT_NW_ACCEL_GRID;
   const size_t gbytes = use_grid ? grid_bytes(ctx) : 0;
-  // spheres-only scene on the one-wave-per-item kernel (A/B)
-  const bool simple_np = use_grid && ctx->simple && ctx->simple_ok && ctx->simple_gridk && gbytes <= kLdsBudget;
-  const bool persist = !simple_np && RTMI_NW_PERSIST && ctx->persist_blocks > 0 &&
+  const bool persist = RTMI_NW_PERSIST && ctx->persist_blocks > 0 &&
                        (use_grid || (ctx->nnodes > 0 && node_bytes <= kPLdsBudget));
   // the spheres-only instantiation of the persistent grid kernel
   const bool simple = persist && use_grid && ctx->simple && ctx->simple_ok && ctx->persist_blocks_simple > 0;
@@ -835,19 +808,16 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
   const size_t lds = use_grid ? gbytes
                      : persist ? (p_objs ? node_bytes + obj_bytes : node_bytes)
                                : lds_objs ? node_bytes + obj_bytes : lds_nodes ? node_bytes : 0;
-  const unsigned blocks = persist     ? unsigned(std::min<int64_t>(pblocks, (a.n_items + pwaves - 1) / pwaves))
-                          : simple_np ? unsigned((a.n_items + RTMI_NW_SG_WAVES - 1) / RTMI_NW_SG_WAVES)
-                                      : unsigned((a.n_items + kWaves - 1) / kWaves);
+  const unsigned blocks = persist ? unsigned(std::min<int64_t>(pblocks, (a.n_items + pwaves - 1) / pwaves))
+                                  : unsigned((a.n_items + kWaves - 1) / kWaves);
   if (persist) HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
   ctx->last_kernel[0] = persist ? 1 : 0;
   ctx->last_kernel[1] = use_grid ? 1 : 0;
-  ctx->last_kernel[2] = simple || simple_np ? 1 : 0;
+  ctx->last_kernel[2] = simple ? 1 : 0;
   ctx->last_kernel[3] = a.chunk;
   auto launch = [&](auto chunked) {
     constexpr bool C = decltype(chunked)::value;
-    if (simple_np)
-      hipLaunchKernelGGL((render_kernel_simple<C>), dim3(blocks), dim3(64 * RTMI_NW_SG_WAVES), lds, st, v, a, ctx->accum, dev_strip, ctx->segments);
-    else if (simple)
+    if (simple)
       hipLaunchKernelGGL((render_persistent<C, true, true, true>), dim3(blocks), dim3(64 * persist_waves<true>()), lds, st, v, a, ctx->accum, dev_strip, ctx->segments, ctx->counter);
     else if (persist && use_grid)
       hipLaunchKernelGGL((render_persistent<C, true, true>), dim3(blocks), dim3(64 * kPWaves), lds, st, v, a, ctx->accum, dev_strip, ctx->segments, ctx->counter);

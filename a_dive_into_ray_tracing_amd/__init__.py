@@ -348,6 +348,68 @@ def render_multi(W, H, spp, max_depth, world, cam, seed=1984, n_gpus=0):
     return out.reshape(H, W, 3)
 
 
+class MultiRenderer:
+    """rt_multi_*: one context per device with the scene resident and one
+    RCCL communicator, reused by every render (include/rtmi.h)."""
+
+    def __init__(self, world, n_gpus=0):
+        self.L = load()
+        self._h = C.c_void_p()
+        sc = world.c_struct()
+        check(self.L.rt_multi_create(C.byref(sc), n_gpus, C.byref(self._h)), "rt_multi_create")
+        n = C.c_int32()
+        check(self.L.rt_multi_device_count(self._h, C.byref(n)), "rt_multi_device_count")
+        self.n_gpus = n.value
+        self._size = None
+
+    def render(self, cam, W, H, spp, max_depth=50, seed=1984):
+        out = np.zeros(W * H * 3, np.float32)
+        check(self.L.rt_multi_render(self._h, C.byref(cam), W, H, spp, max_depth, seed, out.ctypes.data_as(_fp)),
+              "rt_multi_render")
+        return out.reshape(H, W, 3)
+
+    def last_timing(self):
+        """(per-device strip ms, gather ms) of the last render / resolve."""
+        ms = np.zeros(self.n_gpus, np.float32)
+        g = C.c_float()
+        check(self.L.rt_multi_last_timing(self._h, ms.ctypes.data_as(_fp), C.byref(g)), "rt_multi_last_timing")
+        return ms.tolist(), g.value
+
+    def accum_reset(self, W, H):
+        check(self.L.rt_multi_accum_reset(self._h, W, H), "rt_multi_accum_reset")
+        self._size = (W, H)
+
+    def render_pass(self, cam, s_begin, s_count, max_depth=50, seed=1984):
+        check(self.L.rt_multi_render_pass(self._h, C.byref(cam), s_begin, s_count, max_depth, seed),
+              "rt_multi_render_pass")
+
+    def accum_resolve(self):
+        W, H = self._size
+        out = np.zeros(W * H * 3, np.float32)
+        check(self.L.rt_multi_accum_resolve(self._h, out.ctypes.data_as(_fp)), "rt_multi_accum_resolve")
+        return out.reshape(H, W, 3)
+
+    def close(self):
+        if self._h:
+            self.L.rt_multi_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def unpermute_rows(strips, H):
+    """rt_unpermute_rows: interleaved strips [G, nrows, W, 3] -> image [H, W, 3]."""
+    s = np.ascontiguousarray(strips, np.float32)
+    G, nrows, W, _ = s.shape
+    out = np.zeros(H * W * 3, np.float32)
+    check(load().rt_unpermute_rows(s.ctypes.data_as(_fp), G, nrows, W, H, out.ctypes.data_as(_fp)), "rt_unpermute_rows")
+    return out.reshape(H, W, 3)
+
+
 def quantize(sums, spp):
     """write_color quantisation color.h:14-28 -> uint8 [H, W, 3], top row first."""
     s = np.ascontiguousarray(sums, np.float32)

@@ -100,6 +100,16 @@ SIGNATURES = {
     ),
     "rt_replay_worker": (C.c_int, [C.c_void_p, C.POINTER(RtCamera)] + [C.c_int32] * 5 + [_ip, _ip, _lp, _dp, _lp]),
     "rt_render_multi": (C.c_int, [C.POINTER(RtScene), C.POINTER(RtCamera)] + [C.c_int32] * 4 + [C.c_uint64, C.c_int32, _fp]),
+    "rt_multi_create": (C.c_int, [C.POINTER(RtScene), C.c_int32, C.POINTER(C.c_void_p)]),
+    "rt_multi_destroy": (C.c_int, [C.c_void_p]),
+    "rt_multi_device_count": (C.c_int, [C.c_void_p, _ip]),
+    "rt_multi_context": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]),
+    "rt_multi_render": (C.c_int, [C.c_void_p, C.POINTER(RtCamera)] + [C.c_int32] * 4 + [C.c_uint64, _fp]),
+    "rt_multi_last_timing": (C.c_int, [C.c_void_p, _fp, _fp]),
+    "rt_multi_accum_reset": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    "rt_multi_render_pass": (C.c_int, [C.c_void_p, C.POINTER(RtCamera)] + [C.c_int32] * 3 + [C.c_uint64]),
+    "rt_multi_accum_resolve": (C.c_int, [C.c_void_p, _fp]),
+    "rt_unpermute_rows": (C.c_int, [_fp] + [C.c_int32] * 4 + [_fp]),
     # include/rtmi_nw.h (Next-Week renderer)
     "rt_nw_camera_init": (C.c_int, [C.POINTER(RtNwCamera), _dp, _dp, _dp] + [C.c_double] * 6),
     "rt_nw_scene_create": (C.c_int, [C.POINTER(C.c_void_p)]),

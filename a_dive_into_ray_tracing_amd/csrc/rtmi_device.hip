@@ -1066,9 +1066,9 @@ struct rt_ctx {
   int32_t nbvh_sph = 0;
   int32_t resident_blocks_bvh = 0;  // persistent grid with the BVH's LDS
   // uniform grid, built by rt_ctx_set_scene beside the BVH
-  float4 *grid_sph = nullptr;
-  int32_t *grid_idx = nullptr;
-  uint16_t *grid_cell_start = nullptr, *grid_refs = nullptr;
+  float4 *grid_sph = nullptr;  // every sphere by scene index
+  uint32_t *grid_cells = nullptr;  // per cell: first | end << 16 into grid_refs
+  uint16_t *grid_refs = nullptr;   // scene indices
   GridDesc grid{};
   int32_t ngrid_sph = 0;
   bool grid_ok = false;
@@ -1213,8 +1213,7 @@ RTMI_EXPORT int rt_ctx_destroy(rt_ctx *ctx) {
                   (void *)ctx->sh164, (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments, (void *)ctx->pairs, (void *)ctx->counter, (void *)ctx->pass_accum,
                   (void *)ctx->big_pairs, (void *)ctx->big_idx, (void *)ctx->nodes, (void *)ctx->bvh_sph, (void *)ctx->bvh_idx,
                   (void *)ctx->cost_prev, (void *)ctx->cost_cur, (void *)ctx->cost_sorted, (void *)ctx->order,
-                  (void *)ctx->iota, ctx->sort_tmp, (void *)ctx->grid_sph, (void *)ctx->grid_idx,
-                  (void *)ctx->grid_cell_start, (void *)ctx->grid_refs})
+                  (void *)ctx->iota, ctx->sort_tmp, (void *)ctx->grid_sph, (void *)ctx->grid_cells, (void *)ctx->grid_refs})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(ctx->stream);
   if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
@@ -1339,11 +1338,12 @@ namespace {
 // a rounding error far below the margins.
 struct GridBuild {
   GridDesc desc{};
-  std::vector<float4> sph;
-  std::vector<int32_t> idx;
-  std::vector<uint16_t> cell_start, refs;
+  std::vector<float4> sph;     // every sphere of the scene by scene index
+  std::vector<uint32_t> cells;  // per cell: first | end << 16
+  std::vector<uint16_t> refs;   // scene indices
 };
-bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, GridBuild &out) {
+bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, int32_t n, GridBuild &out) {
+  if (n > 65535) return false;  // references are 16-bit scene indices
   const char *env = std::getenv("RTMI_GRID_CELLS");
   // 0.3 cells per sphere: config 2 33.3 ms (0.2: 33.3, 0.5: 33.6, 1: 34.5,
   // 2: 35.2, 4: 38.0; profiles/r02/grid_sweep)
@@ -1381,8 +1381,7 @@ bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, GridBuil
   }
   out.desc.ncells = int32_t(total);
   std::vector<std::vector<uint16_t>> lists(static_cast<size_t>(total));
-  for (size_t s = 0; s < small.size(); ++s) {
-    const int32_t k = small[s];
+  for (int32_t k : small) {  // ascending scene index
     const double *c = b.cr + 4 * k, R = std::fabs(c[3]) + b.margin(k);
     int c0[3], c1[3];
     for (int a = 0; a < 3; ++a) {
@@ -1394,32 +1393,18 @@ bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, GridBuil
     for (int z = c0[2]; z <= c1[2]; ++z)
       for (int y = c0[1]; y <= c1[1]; ++y)
         for (int x = c0[0]; x <= c1[0]; ++x)
-          lists[size_t(x + out.desc.n[0] * (y + out.desc.n[1] * z))].push_back(uint16_t(s));
-    out.sph.push_back(b.g[k]);
-    out.idx.push_back(k);
+          lists[size_t(x + out.desc.n[0] * (y + out.desc.n[1] * z))].push_back(uint16_t(k));
   }
-  out.cell_start.resize(size_t(total) + 1);
+  // the LDS sphere array: the scene's spheres at their scene indices
+  out.sph.assign(b.g.begin(), b.g.begin() + n);
+  out.cells.resize(size_t(total));
   for (int64_t cidx = 0; cidx < total; ++cidx) {
-    out.cell_start[size_t(cidx)] = uint16_t(out.refs.size());
+    const size_t first = out.refs.size();
     out.refs.insert(out.refs.end(), lists[size_t(cidx)].begin(), lists[size_t(cidx)].end());
     if (out.refs.size() > 65535) return false;
+    out.cells[size_t(cidx)] = uint32_t(first) | uint32_t(out.refs.size()) << 16;
   }
-  out.cell_start[size_t(total)] = uint16_t(out.refs.size());
   out.desc.nrefs = int32_t(out.refs.size());
-#if RTMI_GRID_DIRECT
-  {  // each cell's spheres stored contiguously: sphere data per reference
-    std::vector<float4> sph;
-    std::vector<int32_t> idx;
-    for (uint16_t slot : out.refs) {
-      sph.push_back(out.sph[slot]);
-      idx.push_back(out.idx[slot]);
-    }
-    out.sph.swap(sph);
-    out.idx.swap(idx);
-    out.refs.clear();
-    out.desc.nrefs = 0;
-  }
-#endif
   return grid_lds_bytes(int32_t(out.sph.size()), out.desc.ncells, out.desc.nrefs) <= kBvhLdsMax;
 }
 }  // namespace
@@ -1568,19 +1553,16 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
     // uniform grid over the same small spheres
     ctx->grid_ok = false;
     GridBuild gb;
-    if (!small.empty() && n <= 65535 && build_grid(b, small, gb)) {
-      if ((rc = dev_alloc(&ctx->grid_sph, gb.sph.size())) || (rc = dev_alloc(&ctx->grid_idx, gb.idx.size())) ||
-          (rc = dev_alloc(&ctx->grid_cell_start, gb.cell_start.size())) ||
+    if (!small.empty() && build_grid(b, small, n, gb)) {
+      if ((rc = dev_alloc(&ctx->grid_sph, gb.sph.size())) || (rc = dev_alloc(&ctx->grid_cells, gb.cells.size())) ||
           (rc = dev_alloc(&ctx->grid_refs, std::max<size_t>(gb.refs.size(), 1))))
         return rc;
       HIP_TRY(hipMemcpy(ctx->grid_sph, gb.sph.data(), gb.sph.size() * sizeof(float4), hipMemcpyHostToDevice));
-      HIP_TRY(hipMemcpy(ctx->grid_idx, gb.idx.data(), gb.idx.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-      HIP_TRY(hipMemcpy(ctx->grid_cell_start, gb.cell_start.data(), gb.cell_start.size() * sizeof(uint16_t),
-                        hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(ctx->grid_cells, gb.cells.data(), gb.cells.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
       if (!gb.refs.empty())
         HIP_TRY(hipMemcpy(ctx->grid_refs, gb.refs.data(), gb.refs.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
       ctx->grid = gb.desc;
-      ctx->grid.cell_start = ctx->grid_cell_start;
+      ctx->grid.cells = ctx->grid_cells;
       ctx->grid.refs = ctx->grid_refs;
       ctx->ngrid_sph = int32_t(gb.sph.size());
       ctx->grid_ok = true;
@@ -1662,7 +1644,6 @@ Accel accel_of(const rt_ctx *ctx, int kind) {
     a.nsph = ctx->nbvh_sph;
   } else if (kind == 2) {
     a.sph = ctx->grid_sph;
-    a.sph_idx = ctx->grid_idx;
     a.nsph = ctx->ngrid_sph;
     a.grid = ctx->grid;
   }

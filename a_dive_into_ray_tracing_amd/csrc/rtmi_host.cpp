@@ -241,6 +241,24 @@ RTMI_EXPORT int rt_write_ppm(const char *path, const float *sum, int32_t W, int3
   return ok ? RT_OK : set_error(RT_EIO, "rt_write_ppm: write to %s failed", path);
 }
 
+// The multi-GPU row partition's inverse: strip g holds image
+// rows g, g + G, g + 2G, ... (rt_render_rows with row0 = g, row_step = G) in
+// nrows rows each; rows >= H are padding.  The reference has no multi-device
+// path (its 16 threads write disjoint slots of one img, main.cpp:318-338).
+RTMI_EXPORT int rt_unpermute_rows(const float *strips, int32_t n_strips, int32_t nrows, int32_t W, int32_t H,
+                                  float *image) {
+  if (!strips || !image || n_strips < 1 || nrows < 0 || W < 1 || H < 1)
+    return set_error(RT_EINVAL, "rt_unpermute_rows: bad argument");
+  if (int64_t(n_strips) * nrows < H)
+    return set_error(RT_EINVAL, "rt_unpermute_rows: %d strips of %d rows cannot hold %d rows", n_strips, nrows, H);
+  const size_t row = size_t(W) * 3;
+  for (int32_t j = 0; j < H; ++j) {
+    const int32_t g = j % n_strips, k = j / n_strips;
+    std::memcpy(image + size_t(j) * row, strips + (size_t(g) * size_t(nrows) + size_t(k)) * row, row * sizeof(float));
+  }
+  return RT_OK;
+}
+
 // PFM ("PF", 3 channels): the pre-gamma mean sum/spp, little-endian (scale
 // -1), rows bottom to top — the PFM row order is the image's own (row 0 =
 // bottom, main.cpp:274), so rows go out in index order.  SURVEY §8(c) item 5.

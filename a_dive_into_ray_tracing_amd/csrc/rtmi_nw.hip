@@ -437,7 +437,7 @@ struct rt_nw_ctx {
   int32_t nobj = 0, nnodes = 0, ninst = 0, nmat = 0, ntex = 0;
   // uniform grid: descriptor, global arrays, brute-force list
   bool grid_ok = false;
-  GridDesc grid{};
+  NwGridDesc grid{};
   int32_t grid_max_cell = 0;
   uint16_t *grid_cells = nullptr, *grid_refs = nullptr;
   int32_t *grid_big = nullptr;
@@ -651,7 +651,7 @@ RTMI_EXPORT int rt_nw_ctx_set_scene(rt_nw_ctx *ctx, rt_nw_scene *s) {
         (rc = alloc_copy(&ctx->grid_refs, ds.grid_refs.data(), ds.grid_refs.size())) ||
         (rc = alloc_copy(&ctx->grid_big, ds.grid_big.data(), ds.grid_big.size())))
       return rc;
-    GridDesc &G = ctx->grid;
+    NwGridDesc &G = ctx->grid;
     for (int a = 0; a < 3; ++a) {
       G.g0[a] = ds.grid_g0[a];
       G.h[a] = ds.grid_h[a];
@@ -670,7 +670,7 @@ RTMI_EXPORT int rt_nw_ctx_set_scene(rt_nw_ctx *ctx, rt_nw_scene *s) {
     for (int32_t b : ds.grid_big)
       if (b < 0 || size_t(b) >= ds.obj.size()) return set_error(RT_EINVAL, "rt_nw: brute-force index out of range");
   } else {
-    ctx->grid = GridDesc{};
+    ctx->grid = NwGridDesc{};
     ctx->nbig = 0;
     ctx->grid_max_cell = 0;
   }

@@ -103,6 +103,16 @@ __device__ __forceinline__ float nw_acosf(float x) {
 // ---------------------------------------------------------------------------
 // scene view
 // ---------------------------------------------------------------------------
+// The Next-Week grid's descriptor: cell c lists
+// refs[cell_start[c]] .. refs[cell_start[c+1]] (16-bit leaf-order slots).
+struct NwGridDesc {
+  float g0[3], h[3], inv_h[3], g1[3];  // origin, cell size, 1/h, far corner
+  int32_t n[3];
+  int32_t ncells, nrefs;
+  const uint16_t *cell_start;  // ncells + 1
+  const uint16_t *refs;
+};
+
 struct View {
   const DevObj *obj;  // non-media objects, BVH leaf order
   const int32_t *obj_id;
@@ -123,7 +133,7 @@ struct View {
   // uniform grid over the objects (RT_NW_ACCEL_GRID): its
   // descriptor (cell_start / refs: global copies) and the objects tested
   // brute force beside it (leaf-order slots)
-  GridDesc grid;
+  NwGridDesc grid;
   const int32_t *gbig;
   int32_t nbig;
 };
@@ -473,7 +483,7 @@ __device__ __forceinline__ int32_t hit_world_nw_grid(const View &sc, V o, V d, f
   const DevObj *objs = reinterpret_cast<const DevObj *>(nw_nodes_lds);
   const int32_t *oids = reinterpret_cast<const int32_t *>(nw_nodes_lds + 3 * sc.nobj);
   const uint16_t *cs = reinterpret_cast<const uint16_t *>(oids + sc.nobj);
-  const GridDesc &G = sc.grid;
+  const NwGridDesc &G = sc.grid;
   const uint16_t *refs = cs + G.ncells + 1;
   const int32_t *big = reinterpret_cast<const int32_t *>(
       reinterpret_cast<const char *>(cs) + ((size_t(G.ncells) + 1 + size_t(G.nrefs)) * 2 + 3) / 4 * 4);

@@ -13,36 +13,14 @@
 
 #include "../../include/rtmi.h"
 
-#ifndef RTMI_PREFETCH
-#define RTMI_PREFETCH 0
-#endif
 #ifndef RTMI_STATS
 #define RTMI_STATS 0
-#endif
-#ifndef RTMI_DISC_ONLY
-#define RTMI_DISC_ONLY 1
-#endif
-#ifndef RTMI_GRID_UNROLL2
-#define RTMI_GRID_UNROLL2 0
-#endif
-// RTMI_GRID_DIRECT: the grid stores each cell's spheres contiguously (a
-// sphere listed in several cells is stored in each), so a cell-sphere test
-// reads its sphere directly instead of through a 16-bit reference
-#ifndef RTMI_GRID_DIRECT
-#define RTMI_GRID_DIRECT 0
-#endif
-// Fast-mode seeding: s0 = mix64(seed ^ key*phi), s1 = mix64(s0 + phi) — the
-// splitmix64 construction with the (pixel, sample) key as its counter; one
-// 64-bit multiply instead of a third mix64 (the oracle's xo_init is the same;
-// 0 selects the round-1 three-mix64 seeding, for A/B only)
-#ifndef RTMI_CHEAP_SEED
-#define RTMI_CHEAP_SEED 1
 #endif
 
 namespace rtmi {
 
 
-constexpr int kGeomPad = 16;  // zero spheres after the scene: prefetch reads past n stay in bounds
+constexpr int kGeomPad = 16;  // zero spheres after the scene's geom records (padding)
 
 // ---------------------------------------------------------------------------
 // numeric policy
@@ -115,12 +93,10 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 struct Xoro {
   uint64_t s0, s1;
   __device__ __forceinline__ void init(uint64_t seed, uint64_t pixel, uint32_t sample) {
+    // splitmix64 with the (pixel, sample) key as its counter (the oracle's
+    // xo_init is the same)
     const uint64_t key = (pixel << 24) | uint64_t(sample);
-#if RTMI_CHEAP_SEED
     s0 = mix64(seed ^ (key * 0x9E3779B97F4A7C15ULL));
-#else
-    s0 = mix64(seed ^ mix64(key + 0x9E3779B97F4A7C15ULL));
-#endif
     s1 = mix64(s0 + 0x9E3779B97F4A7C15ULL);
   }
   __device__ __forceinline__ uint64_t next() {
@@ -299,187 +275,6 @@ __device__ __forceinline__ int32_t hit_world(const SceneView<R> &sc, V3<R> o, V3
   return best;
 }
 
-// The fast path's form of hit_world: spheres in groups of G.  The group's
-// {centre, r^2} are wave-uniform scalar loads (s_load_dwordx16 for G = 4),
-// the G discriminants are computed branch-free (independent chains), and the
-// wave takes ONE branch per group when no lane has a candidate — the common
-// case.  The candidate test is the sign-bit form of
-//     !(disc < 0) && !(hb >= 0 && cc >= 0)
-// (skips a subset of what that skips, so every skip stays result-preserving,
-// DESIGN.md §3.2).  Candidates are resolved in sphere order, so ties and the
-// shrinking t_max behave exactly as the sequential loop of hit_world above.
-template <int G>
-__device__ __forceinline__ int32_t hit_world_grouped(const float4 *__restrict__ geom, int32_t n, V3<float> o,
-                                                     V3<float> d, float &t_hit
-#if RTMI_STATS
-                                                     , unsigned *stats
-#endif
-                                                     ) {
-  // Expanded form: per segment K = o.d, aL = a|o|^2,
-  // m2ao = -2a*o; per sphere {c, S = |c|^2 - r^2} in SGPRs:
-  //   hb = K - c.d = (o-c).d,  acc = aL + a*S + m2ao.c = a*(|o-c|^2 - r^2),
-  //   disc = hb*hb - acc
-  // -> 8 FMA-class VALU ops per sphere instead of the literal form's 12.
-  const float a = dot<true>(d, d);
-  const float inv_a = 1.0f / a;
-  const float K = dot<true>(o, d);
-  const float aL = a * dot<true>(o, o);
-  const float n2a = -2.0f * a;
-  const V3<float> m2ao = mk(n2a * o.x, n2a * o.y, n2a * o.z);
-  const float t_min = 0.001f;
-  float t_max = INFINITY;
-  int32_t best = -1;
-  auto resolve = [&](int32_t idx, float hb, float disc) {
-    const float sq = dsqrt(disc);
-    float root = (-hb - sq) * inv_a;
-    bool ok = !(root < t_min || t_max < root);
-    if (!ok) {
-      root = (-hb + sq) * inv_a;
-      ok = !(root < t_min || t_max < root);
-    }
-    if (ok) {
-      t_max = root;
-      best = idx;
-    }
-  };
-  auto test = [&](const float4 s, float &hb, float &disc) -> int {
-    hb = __builtin_fmaf(-s.x, d.x, __builtin_fmaf(-s.y, d.y, __builtin_fmaf(-s.z, d.z, K)));
-    const float acc = __builtin_fmaf(m2ao.x, s.x, __builtin_fmaf(m2ao.y, s.y, __builtin_fmaf(m2ao.z, s.z,
-                                     __builtin_fmaf(a, s.w, aL))));
-    disc = __builtin_fmaf(hb, hb, -acc);
-    return (__float_as_int(hb) | __float_as_int(acc)) & ~__float_as_int(disc);  // < 0: candidate
-  };
-  int32_t k = 0;
-#if RTMI_PREFETCH
-  // software pipeline: group k+G's scalar load is issued before group k is
-  // computed (geom is padded by kGeomPad entries), so its latency hides
-  // behind this group's VALU work instead of stalling the wave.
-  float4 nxt[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) nxt[g] = geom[g];
-#endif
-  for (; k + G <= n; k += G) {
-    float4 s[G];
-#if RTMI_PREFETCH
-#pragma unroll
-    for (int g = 0; g < G; ++g) s[g] = nxt[g];
-#pragma unroll
-    for (int g = 0; g < G; ++g) nxt[g] = geom[k + G + g];
-#else
-#pragma unroll
-    for (int g = 0; g < G; ++g) s[g] = geom[k + g];
-#endif
-    float hb[G], disc[G];
-    int ci[G];
-    int any = 0;
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      ci[g] = test(s[g], hb[g], disc[g]);
-      any |= ci[g];
-    }
-#if RTMI_STATS
-    stats[0] += 1;
-    if (__ballot(any < 0)) stats[1] += 1;
-#endif
-    if (any < 0) {
-#pragma unroll
-      for (int g = 0; g < G; ++g)
-        if (ci[g] < 0) {
-#if RTMI_STATS
-          stats[2] += 1;
-#endif
-          resolve(k + g, hb[g], disc[g]);
-        }
-    }
-  }
-  for (; k < n; ++k) {
-    float hb, disc;
-    if (test(geom[k], hb, disc) < 0) resolve(k, hb, disc);
-  }
-  t_hit = t_max;
-  return best;
-}
-
-// Software-pipelined form of hit_world_grouped (experimental, loopbench):
-// two register sets of G spheres; each set's scalar load is issued right
-// after the previous set's first use has forced its s_waitcnt, so a load
-// lands while the other set is computed (SMEM returns out of order, so a
-// wait covers every load outstanding at that point).
-template <int G>
-__device__ __forceinline__ int32_t hit_world_pipelined(const float4 *__restrict__ geom, int32_t n, V3<float> o,
-                                                       V3<float> d, float &t_hit) {
-  const float a = dot<true>(d, d);
-  const float inv_a = 1.0f / a;
-  const float K = dot<true>(o, d);
-  const float aL = a * dot<true>(o, o);
-  const float n2a = -2.0f * a;
-  const V3<float> m2ao = mk(n2a * o.x, n2a * o.y, n2a * o.z);
-  const float t_min = 0.001f;
-  float t_max = INFINITY;
-  int32_t best = -1;
-  auto resolve = [&](int32_t idx, float hb, float disc) {
-    const float sq = dsqrt(disc);
-    float root = (-hb - sq) * inv_a;
-    bool ok = !(root < t_min || t_max < root);
-    if (!ok) {
-      root = (-hb + sq) * inv_a;
-      ok = !(root < t_min || t_max < root);
-    }
-    if (ok) {
-      t_max = root;
-      best = idx;
-    }
-  };
-  auto test = [&](const float4 s, float &hb, float &disc) -> int {
-    hb = __builtin_fmaf(-s.x, d.x, __builtin_fmaf(-s.y, d.y, __builtin_fmaf(-s.z, d.z, K)));
-    const float acc = __builtin_fmaf(m2ao.x, s.x, __builtin_fmaf(m2ao.y, s.y, __builtin_fmaf(m2ao.z, s.z,
-                                     __builtin_fmaf(a, s.w, aL))));
-    disc = __builtin_fmaf(hb, hb, -acc);
-    return (__float_as_int(hb) | __float_as_int(acc)) & ~__float_as_int(disc);
-  };
-  // compute one set; the next set's loads are issued after this set's first
-  // test (which carries the wait for this set)
-  auto group = [&](const float4 (&cur)[G], float4 (&nxt)[G], int32_t k, int32_t knext) {
-    float hb[G], disc[G];
-    int ci[G];
-    ci[0] = test(cur[0], hb[0], disc[0]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int g = 0; g < G; ++g) nxt[g] = geom[knext + g];
-    __builtin_amdgcn_sched_barrier(0);
-    int any = ci[0];
-#pragma unroll
-    for (int g = 1; g < G; ++g) {
-      ci[g] = test(cur[g], hb[g], disc[g]);
-      any |= ci[g];
-    }
-    if (any < 0) {
-#pragma unroll
-      for (int g = 0; g < G; ++g)
-        if (ci[g] < 0) resolve(k + g, hb[g], disc[g]);
-    }
-  };
-  float4 A[G], B[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) A[g] = geom[g];
-  int32_t k = 0;
-  for (; k + 2 * G <= n; k += 2 * G) {
-    group(A, B, k, k + G);          // loads B while A is tested
-    group(B, A, k + G, k + 2 * G);  // loads the next A (geom is padded)
-  }
-  if (k + G <= n) {
-    float4 dummy[G];
-    group(A, dummy, k, k + G);
-    k += G;
-  }
-  for (; k < n; ++k) {
-    float hb, disc;
-    if (test(geom[k], hb, disc) < 0) resolve(k, hb, disc);
-  }
-  t_hit = t_max;
-  return best;
-}
-
 // Packed form (the production loop).  On gfx950 a VALU op that reads an
 // SGPR issues at HALF rate (4.07 vs 2.15 cycles per wave64 instruction,
 // tools/valubench2.hip), while v_pk_fma_f32 — two FMAs per lane — issues at
@@ -488,7 +283,7 @@ __device__ __forceinline__ int32_t hit_world_pipelined(const float4 *__restrict_
 // (SoA within the pair, 32 B), the ray terms are broadcast to both halves,
 // and each of the 8 FMA-class ops per sphere becomes half of one
 // v_pk_fma_f32.  Each half is an IEEE fma, so results are bit-identical to
-// hit_world_grouped (and to the oracle).  Scenes are padded to a multiple of
+// the scalar loop hit_world (and to the oracle).  Scenes are padded to a multiple of
 // 2*GP spheres with a dummy {0, 0, 0, 1e30} that can never be a candidate.
 typedef float f2v __attribute__((ext_vector_type(2)));
 struct SpherePair {
@@ -530,50 +325,23 @@ __device__ __forceinline__ int32_t hit_world_packed(const SpherePair *__restrict
       best = idx;
     }
   };
-#if RTMI_PREFETCH
-  // software pipeline (see hit_world_pipelined): the next group's scalar
-  // loads are issued right after this group's first pk_fma has forced the
-  // wait for this group, so they land while this group is computed.
-  SpherePair nxt[GP];
-#pragma unroll
-  for (int g = 0; g < GP; ++g) nxt[g] = pairs[g];
-#endif
   for (int32_t q = 0; q < npairs; q += GP) {
     SpherePair p[GP];
-#if RTMI_PREFETCH
-#pragma unroll
-    for (int g = 0; g < GP; ++g) p[g] = nxt[g];
-    f2v h0 = __builtin_elementwise_fma(-p[0].cz, DZ, KK);
-    asm volatile("" ::"v"(h0) : "memory");  // h0 (and so the wait for p) before the next loads
-#pragma unroll
-    for (int g = 0; g < GP; ++g) nxt[g] = pairs[q + GP + g];  // padded by GP pairs
-    asm volatile("" ::: "memory");
-#else
 #pragma unroll
     for (int g = 0; g < GP; ++g) p[g] = pairs[q + g];
-#endif
     f2v hb[GP], disc[GP];
     int ci[2 * GP];
     int any = 0;
 #pragma unroll
     for (int g = 0; g < GP; ++g) {
-#if RTMI_PREFETCH
-      const f2v hz = g == 0 ? h0 : __builtin_elementwise_fma(-p[g].cz, DZ, KK);
-#else
       const f2v hz = __builtin_elementwise_fma(-p[g].cz, DZ, KK);
-#endif
       hb[g] = __builtin_elementwise_fma(-p[g].cx, DX, __builtin_elementwise_fma(-p[g].cy, DY, hz));
       const f2v acc = __builtin_elementwise_fma(MX, p[g].cx, __builtin_elementwise_fma(MY, p[g].cy,
                       __builtin_elementwise_fma(MZ, p[g].cz, __builtin_elementwise_fma(AA, p[g].S, AL))));
       disc[g] = __builtin_elementwise_fma(hb[g], hb[g], -acc);
-#if RTMI_DISC_ONLY
       // candidate iff disc >= +0 (sign clear): the full test resolves the rest
       ci[2 * g] = ~__float_as_int(disc[g].x);
       ci[2 * g + 1] = ~__float_as_int(disc[g].y);
-#else
-      ci[2 * g] = (__float_as_int(hb[g].x) | __float_as_int(acc.x)) & ~__float_as_int(disc[g].x);
-      ci[2 * g + 1] = (__float_as_int(hb[g].y) | __float_as_int(acc.y)) & ~__float_as_int(disc[g].y);
-#endif
       any |= ci[2 * g] | ci[2 * g + 1];
     }
 #if RTMI_STATS
@@ -631,14 +399,17 @@ constexpr int kBigGroup = RTMI_BIG_GROUP;  // sphere pairs per step of the big-s
 static_assert(kLeafMax >= 1 && kLeafMax <= 15, "leaf size");
 
 // Uniform grid over the small spheres (RT_ACCEL_GRID): cells
-// of size h over the box g0 + [0, n*h) of the spheres' margin-grown boxes;
-// cell c lists (refs[cell_start[c]] .. refs[cell_start[c+1]]) every sphere
-// whose grown box overlaps it, as 16-bit slots into the grid's sphere array.
+// of size h over the box g0 + [0, n*h) of the spheres' margin-grown boxes.
+// Cell c lists refs[start .. end) (cells[c] = start | end << 16): every
+// sphere whose grown box overlaps it, as 16-bit SCENE indices.  The grid's
+// LDS sphere array holds every sphere of the scene at its scene index (the
+// big spheres' slots unused), so a tie compares scene indices directly and
+// no index table is read.
 struct GridDesc {
   float g0[3], h[3], inv_h[3], g1[3];  // origin, cell size, 1/h, far corner
   int32_t n[3];
   int32_t ncells, nrefs;
-  const uint16_t *cell_start;  // ncells + 1
+  const uint32_t *cells;
   const uint16_t *refs;
 };
 
@@ -648,19 +419,16 @@ struct Accel {
   int32_t nbig_pairs;
   int32_t nnodes;
   const BvhNode *nodes;
-  const float4 *sph;         // BVH spheres in leaf order / grid spheres: {cx, cy, cz, S}
-  const int32_t *sph_idx;    // their scene indices
-  int32_t nsph;
+  const float4 *sph;         // BVH: spheres in leaf order; grid: every sphere by scene index
+  const int32_t *sph_idx;    // BVH: the leaf spheres' scene indices
+  int32_t nsph;              // float4s of sph
   GridDesc grid;             // RT_ACCEL_GRID only
 };
 
+// big_idx through the constant address space: wave-uniform scalar loads
 __device__ __forceinline__ int32_t big_index(const Accel &a, int slot) {
-#if RTMI_BIG_SCALAR
   typedef const __attribute__((address_space(4))) int32_t *cidx_t;
   return ((cidx_t)(size_t)a.big_idx)[slot];
-#else
-  return a.big_idx[slot];
-#endif
 }
 
 // The BVH lives in LDS during a launch (dynamic shared memory, staged by
@@ -682,39 +450,18 @@ __device__ __forceinline__ void stage_bvh(const Accel &g) {
   __syncthreads();
 }
 
-// Grid LDS layout: nsph sphere float4s, then ncells + 1 uint16 cell starts,
-// nrefs uint16 refs, nsph uint16 scene indices (scenes of < 65536 spheres,
-// < 65536 refs).
-#ifndef RTMI_BIG_LDS
-#define RTMI_BIG_LDS 0
-#endif
-// RTMI_BIG_SCALAR: the big spheres and their scene indices (wave-uniform
-// addresses) read with scalar loads through the constant address space
-#ifndef RTMI_BIG_SCALAR
-#define RTMI_BIG_SCALAR 1
-#endif
-constexpr int kBigLdsPairs = 4;  // big-sphere pairs staged after the grid (RTMI_BIG_LDS)
+// Grid LDS layout: nsph sphere float4s (scene order), ncells uint32 cell
+// ranges, nrefs uint16 references (scenes of < 65536 spheres and refs).
 __host__ __device__ constexpr size_t grid_lds_bytes(int32_t nsph, int32_t ncells, int32_t nrefs) {
-  return (size_t(nsph) * 16 + (size_t(ncells) + 1) * 2 + size_t(nrefs) * 2 + size_t(nsph) * 2 + 15) / 16 * 16 +
-         (RTMI_BIG_LDS ? kBigLdsPairs * 32 : 0);
+  return size_t(nsph) * 16 + size_t(ncells) * 4 + (size_t(nrefs) * 2 + 15) / 16 * 16;
 }
 
 __device__ __forceinline__ void stage_grid(const Accel &g) {
   for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) rtmi_bvh_lds[i] = g.sph[i];
-  uint16_t *u = reinterpret_cast<uint16_t *>(rtmi_bvh_lds + g.nsph);
-  const int nstart = g.grid.ncells + 1;
-  for (int i = threadIdx.x; i < nstart; i += blockDim.x) u[i] = g.grid.cell_start[i];
-  for (int i = threadIdx.x; i < g.grid.nrefs; i += blockDim.x) u[nstart + i] = g.grid.refs[i];
-  for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) u[nstart + g.grid.nrefs + i] = uint16_t(g.sph_idx[i]);
-#if RTMI_BIG_LDS
-  {
-    const size_t off = (size_t(g.nsph) * 16 + (size_t(g.grid.ncells) + 1) * 2 + size_t(g.grid.nrefs) * 2 +
-                        size_t(g.nsph) * 2 + 15) / 16;
-    const float4 *src = reinterpret_cast<const float4 *>(g.big);
-    const int n4 = 2 * (g.nbig_pairs < kBigLdsPairs ? g.nbig_pairs : kBigLdsPairs);
-    for (int i = threadIdx.x; i < n4; i += blockDim.x) rtmi_bvh_lds[off + i] = src[i];
-  }
-#endif
+  uint32_t *c = reinterpret_cast<uint32_t *>(rtmi_bvh_lds + g.nsph);
+  for (int i = threadIdx.x; i < g.grid.ncells; i += blockDim.x) c[i] = g.grid.cells[i];
+  uint16_t *r = reinterpret_cast<uint16_t *>(c + g.grid.ncells);
+  for (int i = threadIdx.x; i < g.grid.nrefs; i += blockDim.x) r[i] = g.grid.refs[i];
   __syncthreads();
 }
 
@@ -723,38 +470,120 @@ __device__ __forceinline__ void stage_grid(const Accel &g) {
 // (v_rcp_f32, ~1 ulp) instead of a correctly rounded division: the
 // structures' margins are ~1e4 times larger than that error, and no hit
 // result depends on it (the sphere tests use the exact inv_a).
-#ifndef RTMI_FAST_RCP
-#define RTMI_FAST_RCP 1
-#endif
 __device__ __forceinline__ float safe_inv(float v) {
   const float c = __builtin_fabsf(v) < 1e-20f ? __builtin_copysignf(1e-20f, v) : v;
-#if RTMI_FAST_RCP
   return __builtin_amdgcn_rcpf(c);
-#else
-  return 1.0f / c;
-#endif
 }
 
-// Closest hit through the uniform grid (RT_ACCEL_GRID, staged in LDS by
-// stage_grid): the big spheres brute force, then a 3D-DDA walk over the
-// cells the ray crosses inside [entry, t_max], testing each cell's spheres
-// with exactly the brute-force arithmetic and the order-independent tie rule.
-// The walk stops at the first cell whose exit lies at or beyond the closest
-// hit so far.  Exact: every sphere is listed in every cell
-// its grown box overlaps, the grow margin (>= 1e-3 of the sphere's scale) is
-// orders of magnitude above the float error of the cell boundaries (each
-// computed directly from the cell index, never accumulated), so the cell the
-// DDA holds for any accepted hit point lists that sphere; a sphere tested in
-// several cells gives the same root each time.
 #ifndef RTMI_TRACE_PHASES
 #define RTMI_TRACE_PHASES 0
 #endif
+
 #if RTMI_TRACE_PHASES
 // analysis only: wave-level cycles (s_memtime) of the grid walk's phases:
 // [0] big spheres, [1] clip + DDA setup, [2] cell walk
 struct PhaseClock { unsigned long long c[3]; };
 #endif
 
+// Per-segment ray terms of the expanded sphere test, shared
+// by the accelerated walks.  Plain scalars, not a struct: a struct here ends
+// up in scratch memory (its fields get combined into vector loads before
+// they can be promoted to registers).
+#define RTMI_RAY_TERMS(o, d)                                    \
+  const float a = dot<true>(d, d);                              \
+  const float inv_a = 1.0f / a;                                 \
+  const float K = dot<true>(o, d);                              \
+  const float aL = a * dot<true>(o, o);                         \
+  const float n2a = -2.0f * a;                                  \
+  const float mx = n2a * o.x, my = n2a * o.y, mz = n2a * o.z;
+
+// sphere {c, S = |c|^2 - r^2}: hb = (o-c).d, disc = hb^2 - a(|o-c|^2 - r^2)
+__device__ __forceinline__ void sphere_test(const float4 sp, V3<float> d, float K, float a, float aL, float mx,
+                                            float my, float mz, float &hb, float &disc) {
+  hb = __builtin_fmaf(-sp.x, d.x, __builtin_fmaf(-sp.y, d.y, __builtin_fmaf(-sp.z, d.z, K)));
+  const float ac = __builtin_fmaf(mx, sp.x, __builtin_fmaf(my, sp.y, __builtin_fmaf(mz, sp.z, __builtin_fmaf(a, sp.w, aL))));
+  disc = __builtin_fmaf(hb, hb, -ac);
+}
+
+// sphere.h:30-38 root logic, closed interval [0.001, t_max]; the reference's
+// "later object wins ties" (hittable_list.h:25-31) made order-independent: a
+// root equal to t_max replaces the hit only for a larger scene index, so any
+// visiting order gives the in-order loop's hit.  The second root counts only
+// when the first is rejected; both are formed and selected (no branch:
+// measured faster than forming the second only when needed).
+__device__ __forceinline__ void resolve_root(int32_t idx, float hb, float disc, float inv_a, float &t_max,
+                                             int32_t &best) {
+  const float sq = dsqrt(disc);
+  const float r1 = (-hb - sq) * inv_a, r2 = (-hb + sq) * inv_a;
+  const bool later = idx > best;
+  const bool ok1 = !(r1 < 0.001f) && (r1 < t_max || (r1 == t_max && later));
+  const bool ok2 = !(r2 < 0.001f) && (r2 < t_max || (r2 == t_max && later));
+  if (ok1 || ok2) {
+    t_max = ok1 ? r1 : r2;
+    best = idx;
+  }
+}
+
+// The big spheres (the ones kept out of the BVH / grid: the R = 1000 ground
+// and the r = 1 spheres) by the packed brute-force loop: group data and scene
+// indices through scalar loads, each half of a v_pk_fma_f32 an IEEE fma.
+template <int GP>
+__device__ __forceinline__ void hit_big(const Accel &acc_s, V3<float> d, float K, float a, float aL, float mx, float my,
+                                        float mz, float inv_a, float &t_max, int32_t &best
+#if RTMI_STATS
+                                        , unsigned *stats
+#endif
+                                        ) {
+  static_assert(GP == 2, "the big-sphere loop resolves groups of two pairs");
+  const f2v DX = {d.x, d.x}, DY = {d.y, d.y}, DZ = {d.z, d.z}, KK = {K, K};
+  const f2v MX = {mx, mx}, MY = {my, my}, MZ = {mz, mz};
+  const f2v AA = {a, a}, AL = {aL, aL};
+  typedef const __attribute__((address_space(4))) SpherePair *cpair_t;
+  const cpair_t cp = (cpair_t)(size_t)acc_s.big;
+  auto pair = [&](int q, f2v &hb, f2v &disc) {
+    const f2v cx = cp[q].cx, cy = cp[q].cy, cz = cp[q].cz, S = cp[q].S;
+    const f2v hz = __builtin_elementwise_fma(-cz, DZ, KK);
+    hb = __builtin_elementwise_fma(-cx, DX, __builtin_elementwise_fma(-cy, DY, hz));
+    const f2v ac = __builtin_elementwise_fma(MX, cx, __builtin_elementwise_fma(MY, cy,
+                   __builtin_elementwise_fma(MZ, cz, __builtin_elementwise_fma(AA, S, AL))));
+    disc = __builtin_elementwise_fma(hb, hb, -ac);
+  };
+  // candidate iff disc >= +0 (sign clear; the dummies never are)
+  auto cand = [](float x, int bit) { return (__float_as_int(x) >= 0 ? 1u : 0u) << bit; };
+  for (int32_t q = 0; q < acc_s.nbig_pairs; q += 2) {
+    f2v hb0, d0, hb1, d1;
+    pair(q, hb0, d0);
+    pair(q + 1, hb1, d1);
+    // one wave-uniform branch per group when no lane has a candidate, then
+    // per slot (measured: resolving one candidate per lane per round, with
+    // the slot picked by selects, is slower)
+    const unsigned m = cand(d0.x, 0) | cand(d0.y, 1) | cand(d1.x, 2) | cand(d1.y, 3);
+    if (m) {
+#if RTMI_STATS
+      if (__lane_id() == __builtin_ctzll(__ballot(1))) stats[4] += 1;
+#endif
+      if (m & 1u) resolve_root(big_index(acc_s, 2 * q), hb0.x, d0.x, inv_a, t_max, best);
+      if (m & 2u) resolve_root(big_index(acc_s, 2 * q + 1), hb0.y, d0.y, inv_a, t_max, best);
+      if (m & 4u) resolve_root(big_index(acc_s, 2 * q + 2), hb1.x, d1.x, inv_a, t_max, best);
+      if (m & 8u) resolve_root(big_index(acc_s, 2 * q + 3), hb1.y, d1.y, inv_a, t_max, best);
+    }
+  }
+}
+
+// Closest hit through the uniform grid (RT_ACCEL_GRID, staged in LDS by
+// stage_grid): the big spheres brute force, then a 3D-DDA walk over the
+// cells the ray crosses inside [entry, t_max], testing each cell's spheres
+// (one LDS read for the cell's reference range, then per sphere its scene
+// index and its record) with exactly the brute-force arithmetic and the
+// order-independent tie rule.  (Measured and not kept: cells padded to
+// records of four references tested unrolled — more VALU work per cell.)  The walk stops at the first cell whose exit
+// lies at or beyond the closest hit so far.  Exact: every
+// sphere is listed in every cell its grown box overlaps, the grow margin
+// (>= 1e-3 of the sphere's scale) is orders of magnitude above the float
+// error of the cell boundaries (each computed directly from the cell index,
+// never accumulated), so the cell the DDA holds for any accepted hit point
+// lists that sphere; a sphere tested in several cells gives the same root
+// each time.
 template <int GP>
 __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> o, V3<float> d, float &t_hit
 #if RTMI_STATS
@@ -767,85 +596,14 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
 #if RTMI_TRACE_PHASES
   const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
 #endif
-  // ray terms of the expanded sphere test (as hit_world_bvh)
-  const float a = dot<true>(d, d);
-  const float inv_a = 1.0f / a;
-  const float K = dot<true>(o, d);
-  const float aL = a * dot<true>(o, o);
-  const float n2a = -2.0f * a;
-  const float mx = n2a * o.x, my = n2a * o.y, mz = n2a * o.z;
-  const float t_min = 0.001f;
+  RTMI_RAY_TERMS(o, d)
   float t_max = INFINITY;
   int32_t best = -1;
-  // sphere.h:30-38 root logic; tie rule order-independent (as hit_world_bvh)
-  auto resolve = [&](int32_t idx, float hb, float disc) {
-    const float sq = dsqrt(disc);
-    float root = (-hb - sq) * inv_a;
-    bool ok = !(root < t_min) && (root < t_max || (root == t_max && idx > best));
-    if (!ok) {
-      root = (-hb + sq) * inv_a;
-      ok = !(root < t_min) && (root < t_max || (root == t_max && idx > best));
-    }
-    if (ok) {
-      t_max = root;
-      best = idx;
-    }
-  };
-  // 1. big spheres: the packed brute-force loop
-  {
-    const f2v DX = {d.x, d.x}, DY = {d.y, d.y}, DZ = {d.z, d.z}, KK = {K, K};
-    const f2v MX = {mx, mx}, MY = {my, my}, MZ = {mz, mz};
-    const f2v AA = {a, a}, AL = {aL, aL};
-#if RTMI_BIG_LDS
-    const SpherePair *big_lds = reinterpret_cast<const SpherePair *>(
-        rtmi_bvh_lds + (size_t(acc_s.nsph) * 16 + (size_t(acc_s.grid.ncells) + 1) * 2 + size_t(acc_s.grid.nrefs) * 2 +
-                        size_t(acc_s.nsph) * 2 + 15) / 16);
+  hit_big<GP>(acc_s, d, K, a, aL, mx, my, mz, inv_a, t_max, best
+#if RTMI_STATS
+              , gstats
 #endif
-    for (int32_t q = 0; q < acc_s.nbig_pairs; q += GP) {
-      SpherePair p[GP];
-#if RTMI_BIG_LDS
-      if (acc_s.nbig_pairs <= kBigLdsPairs) {
-#pragma unroll
-        for (int g = 0; g < GP; ++g) p[g] = big_lds[q + g];
-      } else {
-#pragma unroll
-        for (int g = 0; g < GP; ++g) p[g] = acc_s.big[q + g];
-      }
-#elif RTMI_BIG_SCALAR
-      // uniform addresses through the constant address space: scalar loads
-      // (s_load, scalar cache) instead of per-lane vector loads
-      typedef const __attribute__((address_space(4))) SpherePair *cpair_t;
-      const cpair_t cp = (cpair_t)(size_t)acc_s.big;
-#pragma unroll
-      for (int g = 0; g < GP; ++g) { p[g].cx = cp[q + g].cx; p[g].cy = cp[q + g].cy; p[g].cz = cp[q + g].cz; p[g].S = cp[q + g].S; }
-#else
-#pragma unroll
-      for (int g = 0; g < GP; ++g) p[g] = acc_s.big[q + g];
-#endif
-      f2v hb[GP], disc[GP];
-      int ci[2 * GP];
-      int any = 0;
-#pragma unroll
-      for (int g = 0; g < GP; ++g) {
-        const f2v hz = __builtin_elementwise_fma(-p[g].cz, DZ, KK);
-        hb[g] = __builtin_elementwise_fma(-p[g].cx, DX, __builtin_elementwise_fma(-p[g].cy, DY, hz));
-        const f2v ac = __builtin_elementwise_fma(MX, p[g].cx, __builtin_elementwise_fma(MY, p[g].cy,
-                       __builtin_elementwise_fma(MZ, p[g].cz, __builtin_elementwise_fma(AA, p[g].S, AL))));
-        disc[g] = __builtin_elementwise_fma(hb[g], hb[g], -ac);
-        ci[2 * g] = ~__float_as_int(disc[g].x);
-        ci[2 * g + 1] = ~__float_as_int(disc[g].y);
-        any |= ci[2 * g] | ci[2 * g + 1];
-      }
-      if (any < 0) {
-#pragma unroll
-        for (int g = 0; g < GP; ++g) {
-          if (ci[2 * g] < 0) resolve(big_index(acc_s, 2 * (q + g)), hb[g].x, disc[g].x);
-          if (ci[2 * g + 1] < 0) resolve(big_index(acc_s, 2 * (q + g) + 1), hb[g].y, disc[g].y);
-        }
-      }
-    }
-  }
-  // 2. the grid (staged in LDS by stage_grid)
+  );
 #if RTMI_TRACE_PHASES
   const unsigned long long tp1 = __builtin_amdgcn_s_memtime();
   pc.c[0] += tp1 - tp0;
@@ -864,9 +622,8 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
                                      __builtin_fminf(__builtin_fmaxf(bz0, bz1), t_max));
   if (tnear <= tfar) {
     const float4 *lds_sph = rtmi_bvh_lds;
-    const uint16_t *cs = reinterpret_cast<const uint16_t *>(rtmi_bvh_lds + acc_s.nsph);
-    const uint16_t *refs = cs + G.ncells + 1;
-    const uint16_t *sidx = refs + G.nrefs;
+    const uint32_t *cells = reinterpret_cast<const uint32_t *>(rtmi_bvh_lds + acc_s.nsph);
+    const uint16_t *refs = reinterpret_cast<const uint16_t *>(cells + G.ncells);
     // entry cell: the cell of o + tnear*d, clamped into the grid
     auto cell_of = [&](float p, int ax) {
       const int c = int(__builtin_floorf((p - G.g0[ax]) * G.inv_h[ax]));
@@ -891,44 +648,22 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
       gstats[0] += 1;
       if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[2] += 1;
 #endif
-      const int e = cs[cell + 1];
-#if RTMI_GRID_UNROLL2
-      // two spheres of the cell per iteration (the second predicated off at
-      // an odd end): half the loop control, two independent LDS chains
-      for (int k = cs[cell]; k < e; k += 2) {
-#if RTMI_STATS
-        gstats[1] += 1 + (k + 1 < e);
-        if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[3] += 2;
-#endif
-        const bool has1 = k + 1 < e;
-        const int slot0 = refs[k], slot1 = refs[has1 ? k + 1 : k];
-        const float4 s0 = lds_sph[slot0], s1 = lds_sph[slot1];
-        const float hb0 = __builtin_fmaf(-s0.x, d.x, __builtin_fmaf(-s0.y, d.y, __builtin_fmaf(-s0.z, d.z, K)));
-        const float hb1 = __builtin_fmaf(-s1.x, d.x, __builtin_fmaf(-s1.y, d.y, __builtin_fmaf(-s1.z, d.z, K)));
-        const float ac0 = __builtin_fmaf(mx, s0.x, __builtin_fmaf(my, s0.y, __builtin_fmaf(mz, s0.z, __builtin_fmaf(a, s0.w, aL))));
-        const float ac1 = __builtin_fmaf(mx, s1.x, __builtin_fmaf(my, s1.y, __builtin_fmaf(mz, s1.z, __builtin_fmaf(a, s1.w, aL))));
-        const float disc0 = __builtin_fmaf(hb0, hb0, -ac0), disc1 = __builtin_fmaf(hb1, hb1, -ac1);
-        if (!(disc0 < 0.0f)) resolve(int32_t(sidx[slot0]), hb0, disc0);
-        if (has1 && !(disc1 < 0.0f)) resolve(int32_t(sidx[slot1]), hb1, disc1);
-      }
-#else
-      for (int k = cs[cell]; k < e; ++k) {
+      const uint32_t range = cells[cell];
+      for (uint32_t k = range & 0xFFFFu, e = range >> 16; k < e; ++k) {
 #if RTMI_STATS
         gstats[1] += 1;
         if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[3] += 1;
 #endif
-#if RTMI_GRID_DIRECT
-        const int slot = k;
-#else
-        const int slot = refs[k];
+        const int32_t idx = refs[k];
+        float hb, disc;
+        sphere_test(lds_sph[idx], d, K, a, aL, mx, my, mz, hb, disc);
+        if (!(disc < 0.0f)) {
+#if RTMI_STATS
+          if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
 #endif
-        const float4 sp = lds_sph[slot];
-        const float hb = __builtin_fmaf(-sp.x, d.x, __builtin_fmaf(-sp.y, d.y, __builtin_fmaf(-sp.z, d.z, K)));
-        const float ac = __builtin_fmaf(mx, sp.x, __builtin_fmaf(my, sp.y, __builtin_fmaf(mz, sp.z, __builtin_fmaf(a, sp.w, aL))));
-        const float disc = __builtin_fmaf(hb, hb, -ac);
-        if (!(disc < 0.0f)) resolve(int32_t(sidx[slot]), hb, disc);
+          resolve_root(idx, hb, disc, inv_a, t_max, best);
+        }
       }
-#endif
       const float texit = __builtin_fminf(tnx, __builtin_fminf(tny, tnz));
       if (!(texit < t_max)) break;  // the closest hit so far lies in the cells walked
       if (tnx <= tny && tnx <= tnz) {
@@ -966,64 +701,15 @@ __device__ __forceinline__ int32_t hit_world_bvh(const Accel &acc_s, V3<float> o
                                                  , unsigned *bstats
 #endif
                                                  ) {
-  const float a = dot<true>(d, d);
-  const float inv_a = 1.0f / a;
-  const float K = dot<true>(o, d);
-  const float aL = a * dot<true>(o, o);
-  const float n2a = -2.0f * a;
-  const float mx = n2a * o.x, my = n2a * o.y, mz = n2a * o.z;
-  const float t_min = 0.001f;
+  RTMI_RAY_TERMS(o, d)
   float t_max = INFINITY;
   int32_t best = -1;
-  // sphere.h:30-38 root logic; tie rule order-independent (see above)
-  auto resolve = [&](int32_t idx, float hb, float disc) {
-#if RTMI_STATS
-    if (__lane_id() == __builtin_ctzll(__ballot(1))) bstats[4] += 1;
-#endif
-    const float sq = dsqrt(disc);
-    float root = (-hb - sq) * inv_a;
-    bool ok = !(root < t_min) && (root < t_max || (root == t_max && idx > best));
-    if (!ok) {
-      root = (-hb + sq) * inv_a;
-      ok = !(root < t_min) && (root < t_max || (root == t_max && idx > best));
-    }
-    if (ok) {
-      t_max = root;
-      best = idx;
-    }
-  };
   // 1. big spheres: the packed brute-force loop
-  {
-    const f2v DX = {d.x, d.x}, DY = {d.y, d.y}, DZ = {d.z, d.z}, KK = {K, K};
-    const f2v MX = {mx, mx}, MY = {my, my}, MZ = {mz, mz};
-    const f2v AA = {a, a}, AL = {aL, aL};
-    for (int32_t q = 0; q < acc_s.nbig_pairs; q += GP) {
-      SpherePair p[GP];
-#pragma unroll
-      for (int g = 0; g < GP; ++g) p[g] = acc_s.big[q + g];
-      f2v hb[GP], disc[GP];
-      int ci[2 * GP];
-      int any = 0;
-#pragma unroll
-      for (int g = 0; g < GP; ++g) {
-        const f2v hz = __builtin_elementwise_fma(-p[g].cz, DZ, KK);
-        hb[g] = __builtin_elementwise_fma(-p[g].cx, DX, __builtin_elementwise_fma(-p[g].cy, DY, hz));
-        const f2v acc = __builtin_elementwise_fma(MX, p[g].cx, __builtin_elementwise_fma(MY, p[g].cy,
-                        __builtin_elementwise_fma(MZ, p[g].cz, __builtin_elementwise_fma(AA, p[g].S, AL))));
-        disc[g] = __builtin_elementwise_fma(hb[g], hb[g], -acc);
-        ci[2 * g] = ~__float_as_int(disc[g].x);
-        ci[2 * g + 1] = ~__float_as_int(disc[g].y);
-        any |= ci[2 * g] | ci[2 * g + 1];
-      }
-      if (any < 0) {
-#pragma unroll
-        for (int g = 0; g < GP; ++g) {
-          if (ci[2 * g] < 0) resolve(big_index(acc_s, 2 * (q + g)), hb[g].x, disc[g].x);
-          if (ci[2 * g + 1] < 0) resolve(big_index(acc_s, 2 * (q + g) + 1), hb[g].y, disc[g].y);
-        }
-      }
-    }
-  }
+  hit_big<GP>(acc_s, d, K, a, aL, mx, my, mz, inv_a, t_max, best
+#if RTMI_STATS
+              , bstats
+#endif
+  );
   // 2. the BVH (staged in LDS by stage_bvh), stackless: per-lane walk of the
   // DFS node array with skip links
   const float4 *lds_sph = rtmi_bvh_lds + acc_s.nnodes;
@@ -1070,11 +756,14 @@ __device__ __forceinline__ int32_t hit_world_bvh(const Accel &acc_s, V3<float> o
 #if RTMI_STATS
         if (__lane_id() == __builtin_ctzll(__ballot(1))) bstats[3] += 1;
 #endif
-        const float4 s = lds_sph[k];
-        const float hb = __builtin_fmaf(-s.x, d.x, __builtin_fmaf(-s.y, d.y, __builtin_fmaf(-s.z, d.z, K)));
-        const float acc = __builtin_fmaf(mx, s.x, __builtin_fmaf(my, s.y, __builtin_fmaf(mz, s.z, __builtin_fmaf(a, s.w, aL))));
-        const float disc = __builtin_fmaf(hb, hb, -acc);
-        if (!(disc < 0.0f)) resolve(int32_t(lds_idx[k]), hb, disc);
+        float hb, disc;
+        sphere_test(lds_sph[k], d, K, a, aL, mx, my, mz, hb, disc);
+        if (!(disc < 0.0f)) {
+#if RTMI_STATS
+          if (__lane_id() == __builtin_ctzll(__ballot(1))) bstats[4] += 1;
+#endif
+          resolve_root(int32_t(lds_idx[k]), hb, disc, inv_a, t_max, best);
+        }
       }
     }
     node = (enter || link < 0) ? node + 1 : link;

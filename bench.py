@@ -390,7 +390,7 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
 
-    ev = []
+    ev, gev = [], []
 
     def timed_render(rows=(row0, row_step, nrows), buf=strip):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -406,7 +406,14 @@ def main():
         else:
             r.render_rows(cam, W, H, SPP, DEPTH, SEED, row0, row_step, nrows, strip.data_ptr(), stream.cuda_stream)
         if N > 1:  # the single exchange step: strips -> rank 0 over RCCL/xGMI
+            if record:  # HIP events around the gather on the render's stream (it waits for the slowest rank)
+                g0 = torch.cuda.Event(enable_timing=True)
+                g0.record(stream)
             gathered = rdist.gather_strips(strip if coll.type == "cuda" else strip.cpu(), rank, N, dst=0)
+            if record:
+                g1 = torch.cuda.Event(enable_timing=True)
+                g1.record(stream)
+                gev.append((g0, g1))
 
     for _ in range(args.warmup):
         step(False)
@@ -421,7 +428,7 @@ def main():
     if N > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
+    elapsed = my_elapsed = time.perf_counter() - t0
     if N > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -429,13 +436,24 @@ def main():
 
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     segs = r.last_segments()  # this rank's strip, last render
+    dist_info = None
     if N > 1:
-        t = torch.tensor([segs], dtype=torch.float64, device=coll)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        total_segs = float(t.item())
-        km = torch.tensor([kernel_ms], dtype=torch.float64, device=coll)
-        dist.all_reduce(km, op=dist.ReduceOp.MAX)
-        kernel_ms_max = float(km.item())
+        # per-rank attribution of the step time: each rank's kernel time, its
+        # gather time (from the end of its own render to the end of the
+        # collective: includes waiting for the slowest rank) and its work
+        gather_ms = float(np.mean([a.elapsed_time(b) for a, b in gev]))
+        mine = torch.tensor([kernel_ms, gather_ms, float(segs), my_elapsed], dtype=torch.float64, device=coll)
+        every = [torch.zeros_like(mine) for _ in range(N)]
+        dist.all_gather(every, mine)
+        every = np.array([e.cpu().numpy() for e in every])
+        total_segs = float(every[:, 2].sum())
+        kernel_ms_max = float(every[:, 0].max())
+        dist_info = {"backend": str(dist.get_backend()), "world_size": dist.get_world_size(),
+                     "kernel_ms_per_rank": [round(float(x), 3) for x in every[:, 0]],
+                     "gather_ms_per_rank": [round(float(x), 3) for x in every[:, 1]],
+                     "segments_per_rank": [int(x) for x in every[:, 2]],
+                     "wall_s_per_rank": [round(float(x), 4) for x in every[:, 3]],
+                     "kernel_imbalance": round(float(every[:, 0].max() / every[:, 0].mean()), 4)}
     else:
         total_segs, kernel_ms_max = float(segs), kernel_ms
 
@@ -595,6 +613,8 @@ def main():
             "one_shot": one_shot,
             "vs_baseline_ref": "published CPU rt_in_one_weekend 0.1189 Msamples/s (README.md:16-19)",
         }
+        if dist_info is not None:
+            line["dist"] = dist_info
         if gather_check is not None:
             line["gather_check"] = gather_check
         if N == 1 and not args.no_cpu_baseline:

@@ -135,8 +135,9 @@ int rt_ctx_set_schedule(rt_ctx *ctx, int32_t chunk, int32_t tail_spp, int32_t ta
 /* Kernel shape.  RT_KERNEL_PERSISTENT: a resident grid of waves pulls work
  * items from a global counter and streams paths continuously (two items in
  * flight per wave).  RT_KERNEL_GRID: one wave per work item.
- * RT_KERNEL_AUTO (default): persistent for strips, grid for whole frames.
- * All give bit-identical images. */
+ * RT_KERNEL_AUTO (default): persistent for brute-force strips (RT_ACCEL_NONE
+ * and fewer than 6e6 tile-samples), grid otherwise — the grid and BVH
+ * accelerators always take RT_KERNEL_GRID.  All give bit-identical images. */
 enum { RT_KERNEL_GRID = 0, RT_KERNEL_PERSISTENT = 1, RT_KERNEL_AUTO = 2 };
 int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind);
 
@@ -239,6 +240,40 @@ int rt_replay_worker(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
  * W*H*3).  n_gpus = 0 means all visible devices.  Same image as rt_render. */
 int rt_render_multi(const rt_scene *scene, const rt_camera *cam, int32_t W, int32_t H,
                     int32_t spp, int32_t max_depth, uint64_t seed, int32_t n_gpus, float *sum);
+
+/* The same with everything kept across renders: rt_multi_create makes one
+ * context per device 0..n_gpus-1 (0 = all visible; RT_ENODEVICE if more are
+ * asked than visible) with the scene resident, and the RCCL communicator
+ * (ncclCommInitAll) once; rt_multi_render reuses them (strips and the gather
+ * buffer grow as needed).  rt_multi_last_timing reports the last render's
+ * per-device strip time (HIP events around each device's rt_render_rows,
+ * strip_ms[n_gpus]) and the gather alone (device 0 waits for every strip
+ * before the gather's start event), in ms.  Progressive passes on N GPUs:
+ * rt_multi_accum_reset(W, H), any number of rt_multi_render_pass over
+ * sample ranges (each device adds its rows' samples to its own fixed-point
+ * accumulator), then rt_multi_accum_resolve gathers the sums (same bits as
+ * one rt_render of the covered samples).  rt_multi_context exposes device
+ * g's context (tuning, accelerator, counters). */
+typedef struct rt_multi rt_multi;
+int rt_multi_create(const rt_scene *scene, int32_t n_gpus, rt_multi **out);
+int rt_multi_destroy(rt_multi *m);
+int rt_multi_device_count(rt_multi *m, int32_t *n);
+int rt_multi_context(rt_multi *m, int32_t g, rt_ctx **ctx);
+int rt_multi_render(rt_multi *m, const rt_camera *cam, int32_t W, int32_t H, int32_t spp,
+                    int32_t max_depth, uint64_t seed, float *sum);
+int rt_multi_last_timing(rt_multi *m, float *strip_ms, float *gather_ms);
+int rt_multi_accum_reset(rt_multi *m, int32_t W, int32_t H);
+int rt_multi_render_pass(rt_multi *m, const rt_camera *cam, int32_t s_begin, int32_t s_count,
+                         int32_t max_depth, uint64_t seed);
+int rt_multi_accum_resolve(rt_multi *m, float *sum);
+
+/* Host helper (no GPU): the row partition's inverse.  strips holds n_strips
+ * strips of nrows x W x 3 floats; strip g holds image rows g, g + n_strips,
+ * g + 2*n_strips, ... (rt_render_rows with row0 = g, row_step = n_strips),
+ * rows >= H being padding.  Writes the H x W x 3 image.  RT_EINVAL when
+ * n_strips * nrows < H. */
+int rt_unpermute_rows(const float *strips, int32_t n_strips, int32_t nrows, int32_t W, int32_t H,
+                      float *image);
 
 #ifdef __cplusplus
 }

@@ -77,3 +77,46 @@ def test_unpermute_inverts_partition():
         s[: len(rows)] = img[rows]
         strips.append(s)
     assert np.array_equal(rdist.unpermute(strips, 11), img)
+
+
+@pytest.mark.parametrize("H_,G", [(17, 2), (17, 3), (800, 3), (801, 8), (5, 8), (2160, 8)])
+def test_c_unpermute_rows_inverts_partition(H_, G):
+    """rt_unpermute_rows (the un-permute rt_multi_render runs after its RCCL
+    gather) == dist.unpermute (bench.py's rank 0) == the image, for ragged H
+    and G > 1, with the padded rows of the short strips holding garbage."""
+    import a_dive_into_ray_tracing_amd as rt
+
+    W_ = 7
+    img = np.random.default_rng(H_ * G).random((H_, W_, 3)).astype(np.float32)
+    strips = []
+    for g in range(G):
+        row0, step, nrows = rdist.strip_rows(H_, g, G)
+        s = np.full((nrows, W_, 3), np.nan, np.float32)
+        rows = list(range(row0, H_, step))
+        s[: len(rows)] = img[rows]
+        strips.append(s)
+    assert np.array_equal(rt.unpermute_rows(np.stack(strips), H_), img)
+    assert np.array_equal(rdist.unpermute([np.nan_to_num(s) for s in strips], H_), img)
+
+
+def test_c_unpermute_rows_rejects_short_strips():
+    import a_dive_into_ray_tracing_amd as rt
+
+    with pytest.raises(rt.RTError) as e:
+        rt.unpermute_rows(np.zeros((3, 2, 4, 3), np.float32), 7)  # 3 x 2 rows < 7
+    assert e.value.code == -1
+
+
+def test_multi_refuses_more_gpus_than_visible():
+    """rt_multi_create / rt_render_multi: more GPUs than visible (none here,
+    one on a 1-GPU box) is RT_ENODEVICE, never a smaller render."""
+    import a_dive_into_ray_tracing_amd as rt
+
+    world = rt.random_scene()
+    n = rt.device_count()
+    with pytest.raises(rt.RTError) as e:
+        rt.MultiRenderer(world, n_gpus=n + 1)
+    assert e.value.code == -3
+    with pytest.raises(rt.RTError) as e:
+        rt.render_multi(8, 8, 1, 50, world, rt.final_camera(1.0), n_gpus=n + 1)
+    assert e.value.code == -3

@@ -179,6 +179,27 @@ def test_render_multi_one_gpu_equals_render(final_world, final_renderer):
     assert np.array_equal(a, b)
 
 
+def test_multi_renderer_reuses_contexts_passes_and_times(final_world, final_renderer):
+    """rt_multi_*: contexts, scene and communicator made once and reused by
+    two renders; progressive passes on the device set resolve to the same
+    bits; per-device strip and gather times are reported."""
+    W, H, S = 40, 30, 6
+    cam = rt.final_camera(W / H)
+    want = final_renderer.render(cam, W, H, S, 50, SEED)
+    m = rt.MultiRenderer(final_world, n_gpus=1)
+    try:
+        for _ in range(2):
+            assert np.array_equal(m.render(cam, W, H, S, 50, SEED), want)
+        strip_ms, gather_ms = m.last_timing()
+        assert len(strip_ms) == 1 and strip_ms[0] > 0 and gather_ms >= 0
+        m.accum_reset(W, H)
+        m.render_pass(cam, 0, 2)
+        m.render_pass(cam, 2, 4)
+        assert np.array_equal(m.accum_resolve(), want)
+    finally:
+        m.close()
+
+
 # ---------------------------------------------------- full-size properties -
 @pytest.fixture(scope="module")
 def config2(final_renderer):
@@ -527,29 +548,44 @@ def test_non_finite_sample_colours_are_guarded():
 
 
 # ------------------------------------------------------------ config 5 -----
+C5 = (3840, 2160, 2000)
+C5_ROWS = (0, 1531)  # the bottom row and one through the spheres' band
+
+
 @pytest.fixture(scope="module")
-def config5(final_renderer):
-    """BASELINE config 5: the final scene at 3840x2160 (16:9 camera, the
-    reference's defocus blur), 2000 spp, whole frame on one GPU (~1.7 s)."""
-    W, H, S = 3840, 2160, 2000
+def config5_oracle_rows(final_world):
+    """The oracle's two full-width config-5 rows at full spp (computed once
+    for both accelerators)."""
+    W, H, S = C5
     cam = rt.final_camera(W / H)
-    final_renderer.set_accel("bvh")
+    return {j: O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED, row0=j, row_step=1, nrows=1)[0]
+            for j in C5_ROWS}
+
+
+@pytest.fixture(scope="module", params=["grid", "bvh"])
+def config5(request, final_renderer):
+    """BASELINE config 5: the final scene at 3840x2160 (16:9 camera, the
+    reference's defocus blur), 2000 spp, whole frame on one GPU — through the
+    product's default uniform grid and through the BVH."""
+    W, H, S = C5
+    cam = rt.final_camera(W / H)
+    final_renderer.set_accel(request.param)
     try:
         img = final_renderer.render(cam, W, H, S, 50, SEED)
         sch = final_renderer.last_schedule()
     finally:
         final_renderer.set_accel("none")
-    return cam, img, sch
+    return request.param, cam, img, sch
 
 
-def test_config5_sampled_rows_bit_exact_vs_oracle(config5, final_world):
+def test_config5_sampled_rows_bit_exact_vs_oracle(config5, config5_oracle_rows):
     """Two full-width rows of config 5 (row 0 and row 1531: bottom and the
-    spheres' band) against the oracle at full spp, bit for bit."""
-    cam, img, sch = config5
-    assert sch["bvh"] == 1 and sch["tile_w"] in (8, 16)
-    for j in (0, 1531):
-        want = O.fast_render(o_scene(final_world), o_cam(cam), 3840, 2160, 2000, 50, SEED, row0=j, row_step=1, nrows=1)
-        assert np.array_equal(img[j], want[0]), j
+    spheres' band) against the oracle at full spp, bit for bit, with the grid
+    (the default path) and with the BVH."""
+    accel, cam, img, sch = config5
+    assert sch["bvh"] == {"bvh": 1, "grid": 2}[accel] and sch["tile_w"] in (8, 16)
+    for j in C5_ROWS:
+        assert np.array_equal(img[j], config5_oracle_rows[j]), (accel, j)
 
 
 def test_config5_strip_of_8_equals_frame_rows(config5, final_renderer):
@@ -557,20 +593,23 @@ def test_config5_strip_of_8_equals_frame_rows(config5, final_renderer):
     rows) rendered alone equals those rows of the whole frame; and the frame
     is finite, fully covered and at the expected brightness."""
     torch = pytest.importorskip("torch")
-    cam, img, _ = config5
-    W, H, S, G, g = 3840, 2160, 2000, 8, 3
+    accel, cam, img, _ = config5
+    W, H, S = C5
+    G, g = 8, 3
     nrows = H // G
     strip = torch.full((nrows, W, 3), -1.0, dtype=torch.float32, device="cuda:0")
-    final_renderer.set_accel("bvh")
+    final_renderer.set_accel(accel)
     try:
         final_renderer.render_rows(cam, W, H, S, 50, SEED, g, G, nrows, strip.data_ptr(), 0)
         final_renderer.synchronize()
+        assert final_renderer.last_schedule()["bvh"] == {"bvh": 1, "grid": 2}[accel]
     finally:
         final_renderer.set_accel("none")
     assert np.array_equal(strip.cpu().numpy(), img[g::G])
     assert np.isfinite(img).all() and (img.reshape(H, -1).max(axis=1) > 0).all()
     mean = float(img.mean() / S)
-    record_parity_stats("config5_frame", {"mean_radiance": mean, "rows_checked_vs_oracle": "0, 1531", "strip": "3 of 8"})
+    record_parity_stats(f"config5_frame_{accel}", {"mean_radiance": mean, "rows_checked_vs_oracle": "0, 1531",
+                                                    "strip": "3 of 8"})
     assert 0.3 < mean < 0.9
 
 

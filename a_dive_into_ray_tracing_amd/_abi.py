@@ -145,6 +145,7 @@ SIGNATURES = {
     "rt_nw_ctx_set_accel": (C.c_int, [C.c_void_p, C.c_int32]),
     "rt_nw_scene_grid_stats": (C.c_int, [C.c_void_p, _ip, _ip, _ip, _ip]),
     "rt_nw_debug_phases": (C.c_int, [C.POINTER(C.c_uint64)]),
+    "rt_nw_debug_counters": (C.c_int, [C.POINTER(C.c_uint64)]),
     "rt_nw_ctx_accel_info": (C.c_int, [C.c_void_p, _ip, _ip, _ip, _ip]),
     "rt_nw_render": (C.c_int, [C.c_void_p, C.POINTER(RtNwCamera)] + [C.c_int32] * 4 + [C.c_uint64, _fp]),
     "rt_nw_render_rows": (
@@ -177,8 +178,13 @@ def load():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"librtmi.so not built at {LIB_PATH}: run `make -C a_dive_into_ray_tracing_amd/csrc`")
         L = C.CDLL(LIB_PATH)
+        override = bool(os.environ.get("RTMI_LIBRARY"))  # an A/B build of an older tree may lack newer symbols
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(L, name)
+            fn = getattr(L, name, None)
+            if fn is None:
+                if override:
+                    continue
+                raise ImportError(f"{LIB_PATH} does not export {name} (rebuild it)")
             fn.restype = res
             fn.argtypes = args
         _lib = L

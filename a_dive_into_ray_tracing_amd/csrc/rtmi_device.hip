@@ -1068,7 +1068,7 @@ struct rt_ctx {
   // uniform grid, built by rt_ctx_set_scene beside the BVH
   float4 *grid_sph = nullptr;  // every sphere by scene index
   uint32_t *grid_cells = nullptr;  // per cell: first | end << 16 into grid_refs
-  uint16_t *grid_refs = nullptr;   // scene indices
+  uint32_t *grid_refs = nullptr;   // 16 x scene index (byte offsets into the LDS sphere array)
   GridDesc grid{};
   int32_t ngrid_sph = 0;
   bool grid_ok = false;
@@ -1340,7 +1340,7 @@ struct GridBuild {
   GridDesc desc{};
   std::vector<float4> sph;     // every sphere of the scene by scene index
   std::vector<uint32_t> cells;  // per cell: first | end << 16
-  std::vector<uint16_t> refs;   // scene indices
+  std::vector<uint32_t> refs;   // 16 x scene index
 };
 bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, int32_t n, GridBuild &out) {
   if (n > 65535) return false;  // references are 16-bit scene indices
@@ -1400,7 +1400,7 @@ bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, int32_t 
   out.cells.resize(size_t(total));
   for (int64_t cidx = 0; cidx < total; ++cidx) {
     const size_t first = out.refs.size();
-    out.refs.insert(out.refs.end(), lists[size_t(cidx)].begin(), lists[size_t(cidx)].end());
+    for (uint16_t k : lists[size_t(cidx)]) out.refs.push_back(uint32_t(k) * 16u);
     if (out.refs.size() > 65535) return false;
     out.cells[size_t(cidx)] = uint32_t(first) | uint32_t(out.refs.size()) << 16;
   }
@@ -1560,7 +1560,7 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
       HIP_TRY(hipMemcpy(ctx->grid_sph, gb.sph.data(), gb.sph.size() * sizeof(float4), hipMemcpyHostToDevice));
       HIP_TRY(hipMemcpy(ctx->grid_cells, gb.cells.data(), gb.cells.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
       if (!gb.refs.empty())
-        HIP_TRY(hipMemcpy(ctx->grid_refs, gb.refs.data(), gb.refs.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(ctx->grid_refs, gb.refs.data(), gb.refs.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
       ctx->grid = gb.desc;
       ctx->grid.cells = ctx->grid_cells;
       ctx->grid.refs = ctx->grid_refs;

@@ -82,10 +82,16 @@ template <bool S> constexpr int persist_waves() { return S ? RTMI_NW_SIMPLE_WAVE
 #ifndef RTMI_NW_PERSIST_PER_EU
 #define RTMI_NW_PERSIST_PER_EU 8
 #endif
-// staged bytes per block (nodes, and objects when they fit) that leave room
-// for two blocks per CU beside their 24 KB accumulators (160 KB LDS per CU)
-constexpr size_t kPTwoBlockBudget = 56 * 1024;
-constexpr size_t kPLdsBudget = 136 * 1024;                    // persistent kernel: staged bytes (+ 24 KB accumulators)
+// Dynamic LDS budgets of the persistent kernel, derived from its static LDS
+// (the waves' accumulators and the camera, rounded up to the allocation
+// granule): staged bytes (nodes, and objects when they fit) that leave room
+// for two blocks per CU, and for one (160 KB LDS per CU).  The launch path
+// also checks the kernel's actual static size (hipFuncGetAttributes), so a
+// new __shared__ variable cannot silently push a block past the CU.
+constexpr size_t kCuLds = 160 * 1024;
+constexpr size_t kPStaticLds = (sizeof(unsigned long long) * 3 * 64 * kPWaves + 23 * sizeof(float) + 255) / 256 * 256;
+constexpr size_t kPTwoBlockBudget = kCuLds / 2 - kPStaticLds;
+constexpr size_t kPLdsBudget = kCuLds - kPStaticLds;
 
 // RTMI_NW_PHASES builds (analysis only): wave-level cycles (s_memtime) of a
 // work item's loop passes: [0] closest hit, [1] hit record + texture +
@@ -96,6 +102,11 @@ constexpr size_t kPLdsBudget = 136 * 1024;                    // persistent kern
 #endif
 #if RTMI_NW_PHASES
 __device__ unsigned long long g_nw_phase[4];
+#endif
+#if RTMI_STATS
+// RTMI_STATS build: executed work of the launches since the last
+// rt_nw_debug_counters call — FLOP, node visits, object tests, cell steps
+__device__ unsigned long long g_nw_stats[4];
 #endif
 
 // NaN -> 0, clamped to [-64, 64]: as rtmi_device.hip to_fixed (and the oracle)
@@ -223,6 +234,7 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
   unsigned long long ph[4] = {0, 0, 0, 0}, pa = 0, pb = 0;
   const unsigned long long p_start = __builtin_amdgcn_s_memtime();
 #endif
+  NwCount cnt{0, 0, 0, 0};
   bool active = lane < nq;
   if (active) start(lane);
   int next = 64;
@@ -238,8 +250,8 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
       const uint64_t seg_key = !S && sc.has_media ? rng.next() : 0ull;
       float t;
       int face;
-      const int32_t k = GRID ? hit_world_nw_grid<S>(sc, o, d, time, seg_key, t, face)
-                             : hit_world_nw<LDS_NODES, LDS_OBJS>(sc, o, d, time, seg_key, t, face);
+      const int32_t k = GRID ? hit_world_nw_grid<S>(sc, o, d, time, seg_key, t, face, &cnt)
+                             : hit_world_nw<LDS_NODES, LDS_OBJS>(sc, o, d, time, seg_key, t, face, &cnt);
 #if RTMI_NW_PHASES
       pb = __builtin_amdgcn_s_memtime();
 #endif
@@ -294,6 +306,14 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
   ph[3] = __builtin_amdgcn_s_memtime() - p_start;
   if (lane == __builtin_ctzll(__ballot(1)))
     for (int q = 0; q < 4; ++q) atomicAdd(&g_nw_phase[q], ph[q]);
+#endif
+#if RTMI_STATS
+  atomicAdd(&g_nw_stats[0], cnt.flop);
+  atomicAdd(&g_nw_stats[1], (unsigned long long)cnt.nodes);
+  atomicAdd(&g_nw_stats[2], (unsigned long long)cnt.objects);
+  atomicAdd(&g_nw_stats[3], (unsigned long long)cnt.cells);
+#else
+  (void)cnt;
 #endif
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -460,6 +480,10 @@ struct rt_nw_ctx {
   bool simple = false;
   bool simple_ok = !(std::getenv("RTMI_NW_SIMPLE") && std::getenv("RTMI_NW_SIMPLE")[0] == '0');
   int32_t persist_blocks_simple = 0;
+  int32_t cus = 0;  // compute units of the device
+  // resident blocks per CU of a persistent launch, by (kernel, dynamic LDS
+  // bytes): the occupancy query repeated with the bytes the launch stages
+  std::vector<std::pair<std::pair<const void *, size_t>, int32_t>> occupancy;
   int32_t last_kernel[4] = {0, 0, 0, 0};  // rt_nw_ctx_last_kernel
   // samples per work item forced by RTMI_NW_CHUNK (A/B only; 0 = automatic),
   // read when the context is created
@@ -561,6 +585,7 @@ RTMI_EXPORT int rt_nw_ctx_create(int32_t device, rt_nw_ctx **out) {
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<true, true, true, true>,
                                                          64 * persist_waves<true>(), 0));
     ctx->persist_blocks_simple = per_cu * prop.multiProcessorCount;
+    ctx->cus = prop.multiProcessorCount;
   }
   *out = ctx.release();
   return RT_OK;
@@ -630,7 +655,17 @@ RTMI_EXPORT int rt_nw_ctx_set_scene(rt_nw_ctx *ctx, rt_nw_scene *s) {
   }
   std::vector<float4> pv(ds.perlin_vec.size() / 4);
   std::memcpy(pv.data(), ds.perlin_vec.data(), pv.size() * sizeof(float4));
+  if (ds.grid_ok) {  // (checked before any device buffer is replaced)
+    for (uint16_t r : ds.grid_refs)
+      if (r >= ds.obj.size()) return set_error(RT_EINVAL, "rt_nw: grid reference out of range");
+    for (int32_t b : ds.grid_big)
+      if (b < 0 || size_t(b) >= ds.obj.size()) return set_error(RT_EINVAL, "rt_nw: brute-force index out of range");
+  }
   Guard g(ctx->device);
+  // the context's structures are replaced below: until that completes, no
+  // render may use a mix of old counts and new buffers
+  ctx->nobj = ctx->nmed = ctx->nnodes = 0;
+  ctx->grid_ok = false;
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   int rc;
   if ((rc = alloc_copy(&ctx->obj, dobj.data(), dobj.size())) ||
@@ -645,7 +680,6 @@ RTMI_EXPORT int rt_nw_ctx_set_scene(rt_nw_ctx *ctx, rt_nw_scene *s) {
       (rc = alloc_copy(&ctx->imgd, ds.image.data(), ds.image.size())) ||
       (rc = alloc_copy(&ctx->nodes, split.data(), split.size())))
     return rc;
-  ctx->grid_ok = ds.grid_ok;
   if (ds.grid_ok) {
     if ((rc = alloc_copy(&ctx->grid_cells, ds.grid_cell_start.data(), ds.grid_cell_start.size())) ||
         (rc = alloc_copy(&ctx->grid_refs, ds.grid_refs.data(), ds.grid_refs.size())) ||
@@ -665,15 +699,12 @@ RTMI_EXPORT int rt_nw_ctx_set_scene(rt_nw_ctx *ctx, rt_nw_scene *s) {
     G.refs = ctx->grid_refs;
     ctx->nbig = int32_t(ds.grid_big.size());
     ctx->grid_max_cell = ds.grid_max_cell;
-    for (uint16_t r : ds.grid_refs)
-      if (r >= ds.obj.size()) return set_error(RT_EINVAL, "rt_nw: grid reference out of range");
-    for (int32_t b : ds.grid_big)
-      if (b < 0 || size_t(b) >= ds.obj.size()) return set_error(RT_EINVAL, "rt_nw: brute-force index out of range");
   } else {
     ctx->grid = NwGridDesc{};
     ctx->nbig = 0;
     ctx->grid_max_cell = 0;
   }
+  ctx->grid_ok = ds.grid_ok;
   ctx->nobj = int32_t(ds.obj.size());
   ctx->nmed = int32_t(ds.med.size());
   ctx->nnodes = int32_t(ds.nodes.size());
@@ -706,7 +737,11 @@ size_t grid_bytes(const rt_nw_ctx *c) {
   return nw_grid_lds_bytes(c->nobj, c->grid.ncells, c->grid.nrefs, c->nbig);
 }
 int32_t accel_used(const rt_nw_ctx *c) {
-  const bool fits = c->grid_ok && grid_bytes(c) <= kPLdsBudget;
+  // the grid is staged whole: by the persistent kernel (one block per CU)
+  // when it runs, else by the grid kernel's per-block budget; a grid that
+  // fits neither renders with the BVH
+  const bool persist = RTMI_NW_PERSIST && c->persist_blocks_grid > 0;
+  const bool fits = c->grid_ok && grid_bytes(c) <= (persist ? kPLdsBudget : kLdsBudget);
   if (c->accel == RT_NW_ACCEL_GRID) return fits ? RT_NW_ACCEL_GRID : RT_NW_ACCEL_BVH;
   if (c->accel == RT_NW_ACCEL_BVH) return RT_NW_ACCEL_BVH;
   return fits && c->grid_max_cell <= kNwGridMaxCell ? RT_NW_ACCEL_GRID : RT_NW_ACCEL_BVH;
@@ -762,7 +797,7 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
   const size_t node_bytes = size_t(ctx->nnodes) * 32, obj_bytes = size_t(ctx->nobj) * (sizeof(DevObj) + 4);
   const bool use_grid = accel_used(ctx) == RT_NW_ACCEL_GRID;
   const size_t gbytes = use_grid ? grid_bytes(ctx) : 0;
-  const bool persist = RTMI_NW_PERSIST && ctx->persist_blocks > 0 &&
+  const bool persist = RTMI_NW_PERSIST && (use_grid ? ctx->persist_blocks_grid > 0 : ctx->persist_blocks > 0) &&
                        (use_grid || (ctx->nnodes > 0 && node_bytes <= kPLdsBudget));
   // the spheres-only instantiation of the persistent grid kernel
   const bool simple = persist && use_grid && ctx->simple && ctx->simple_ok && ctx->persist_blocks_simple > 0;
@@ -774,15 +809,7 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
   // ms with 8, 433 with 32; at 1024 spp 1215 ms with 24, 1205 with 32, 1308
   // with 8 — the item count, not the size, sets its tail
   // (profiles/r01/session6/nw_chunk.txt).  Grid kernel: 32.
-  int64_t chunk = 32;
-  if (persist) {
-    const int64_t waves = int64_t(pblocks) * pwaves;
-    chunk = std::min<int64_t>(32, std::max<int64_t>(4, int64_t(a.tiles) * spp / (80 * waves)));
-  }
-  a.chunk = std::min<int64_t>(spp, ctx->env_chunk > 0 ? ctx->env_chunk : chunk);
-  a.nch = (spp + a.chunk - 1) / a.chunk;
-  if (int64_t(a.tiles) * a.nch >= (int64_t(1) << 31) - kWaves) return set_error(RT_EINVAL, "render too large");
-  a.n_items = a.tiles * a.nch;
+  // (samples per work item: set below, once the resident grid is known)
   // the context's buffers (accumulator, counters) are shared by every render:
   // a render on another stream first waits for the last one
   if (ctx->last_stream && ctx->last_stream != st) HIP_TRY(hipStreamWaitEvent(st, ctx->last_done, 0));
@@ -808,7 +835,45 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
   const size_t lds = use_grid ? gbytes
                      : persist ? (p_objs ? node_bytes + obj_bytes : node_bytes)
                                : lds_objs ? node_bytes + obj_bytes : lds_nodes ? node_bytes : 0;
-  const unsigned blocks = persist ? unsigned(std::min<int64_t>(pblocks, (a.n_items + pwaves - 1) / pwaves))
+  // the kernel that will run, its static LDS beside the staged bytes, and
+  // (persistent) how many of its blocks stay resident with those bytes
+  const void *kfn = simple ? (const void *)render_persistent<true, true, true, true>
+                    : persist && use_grid ? (const void *)render_persistent<true, true, true>
+                    : persist && p_objs ? (const void *)render_persistent<true, true, false>
+                    : persist ? (const void *)render_persistent<true, false, false>
+                    : g_grid ? (const void *)render_kernel<true, false, false, true>
+                    : lds_objs ? (const void *)render_kernel<true, true, true, false>
+                    : lds_nodes ? (const void *)render_kernel<true, true, false, false>
+                                : (const void *)render_kernel<true, false, false, false>;
+  {
+    hipFuncAttributes fa;
+    HIP_TRY(hipFuncGetAttributes(&fa, kfn));
+    if (fa.sharedSizeBytes + lds > kCuLds)
+      return set_error(RT_EINVAL, "rt_nw: %zu B staged + %zu B static LDS exceed a CU's %zu B", lds,
+                       size_t(fa.sharedSizeBytes), kCuLds);
+  }
+  int32_t resident = pblocks;
+  if (persist) {
+    const auto key = std::make_pair(kfn, lds);
+    auto it = std::find_if(ctx->occupancy.begin(), ctx->occupancy.end(), [&](const auto &e) { return e.first == key; });
+    if (it == ctx->occupancy.end()) {
+      int per_cu = 0;
+      HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, int(64 * pwaves), lds));
+      ctx->occupancy.push_back({key, std::max(1, per_cu) * ctx->cus});
+      it = ctx->occupancy.end() - 1;
+    }
+    resident = it->second;
+  }
+  int64_t chunk = 32;
+  if (persist) {
+    const int64_t waves = int64_t(resident) * pwaves;
+    chunk = std::min<int64_t>(32, std::max<int64_t>(4, int64_t(a.tiles) * spp / (80 * waves)));
+  }
+  a.chunk = std::min<int64_t>(spp, ctx->env_chunk > 0 ? ctx->env_chunk : chunk);
+  a.nch = (spp + a.chunk - 1) / a.chunk;
+  if (int64_t(a.tiles) * a.nch >= (int64_t(1) << 31) - kWaves) return set_error(RT_EINVAL, "render too large");
+  a.n_items = a.tiles * a.nch;
+  const unsigned blocks = persist ? unsigned(std::min<int64_t>(resident, (a.n_items + pwaves - 1) / pwaves))
                                   : unsigned((a.n_items + kWaves - 1) / kWaves);
   if (persist) HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
   ctx->last_kernel[0] = persist ? 1 : 0;
@@ -898,6 +963,24 @@ RTMI_EXPORT int rt_nw_debug_trace(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
 
 // Analysis builds only (RTMI_NW_PHASES): the phase cycle sums since the last
 // call (see g_nw_phase), zeroed after reading; RT_EUNSUPPORTED otherwise.
+// RTMI_STATS build (librtmi_stats.so): the executed-work counters of the
+// launches since the last call (see g_nw_stats), zeroed after reading;
+// RT_EUNSUPPORTED in the product build.
+RTMI_EXPORT int rt_nw_debug_counters(uint64_t *out4) {
+#if RTMI_STATS
+  if (!out4) return set_error(RT_EINVAL, "null");
+  HIP_TRY(hipDeviceSynchronize());
+  unsigned long long v[4] = {0, 0, 0, 0}, z[4] = {0, 0, 0, 0};
+  HIP_TRY(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_nw_stats), sizeof v));
+  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_nw_stats), z, sizeof z));
+  for (int q = 0; q < 4; ++q) out4[q] = v[q];
+  return RT_OK;
+#else
+  (void)out4;
+  return set_error(RT_EUNSUPPORTED, "rt_nw_debug_counters: not an RTMI_STATS build");
+#endif
+}
+
 RTMI_EXPORT int rt_nw_debug_phases(uint64_t *out4) {
 #if RTMI_NW_PHASES
   if (!out4) return set_error(RT_EINVAL, "null");

@@ -348,6 +348,21 @@ __device__ __forceinline__ float medium_uniform(uint64_t seg_key, int32_t id, in
   return float(uint32_t(h >> 40) + 1u) * 0x1p-24f;
 }
 
+// Executed-work counters of the RTMI_STATS build (per lane, added to
+// g_nw_stats when an item ends; rt_nw_debug_counters): the algorithmic FLOP of
+// every miss test the walk performs — bench.py NW_FLOP's per-kind counts
+// (sphere 18, moving sphere 30, rectangle 6, box 36, +15 for an instance's
+// ray transform, a medium 2 x its boundary + 4) plus 25 per BVH node slab
+// test or grid-box clip and 5 per grid cell step — and the visits.
+struct NwCount {
+  unsigned long long flop;
+  unsigned nodes, objects, cells;
+};
+__device__ __forceinline__ unsigned nw_test_flop(int kind, bool inst) {
+  const unsigned f = kind == kSphere ? 18u : kind == kMovingSphere ? 30u : kind == kBox ? 36u : 6u;
+  return f + (inst ? 15u : 0u);
+}
+
 // One non-medium object's hit (world ray in; t_min = 0.001, no upper bound:
 // the caller applies the order-independent closest rule).  face: box side.
 // invw = 1/dw per axis of the world ray (hit_rect_inv).
@@ -396,7 +411,7 @@ __device__ __forceinline__ bool hit_object(const View &sc, const DevObj &ob, V o
 extern __shared__ float4 nw_nodes_lds[];
 template <bool LDS_NODES, bool LDS_OBJS>
 __device__ __forceinline__ int32_t hit_world_nw(const View &sc, V o, V d, float time, uint64_t seg_key, float &best_t,
-                                                int &best_face) {
+                                                int &best_face, NwCount *cnt = nullptr) {
   const float4 *nlo = LDS_NODES ? nw_nodes_lds : sc.nlo;
   const float4 *nhi = LDS_NODES ? nw_nodes_lds + sc.nnodes : sc.nhi;
   const DevObj *objs = LDS_OBJS ? reinterpret_cast<const DevObj *>(nw_nodes_lds + 2 * sc.nnodes) : sc.obj;
@@ -412,6 +427,7 @@ __device__ __forceinline__ int32_t hit_world_nw(const View &sc, V o, V d, float 
     V lo = o, ld = d;
     if (ob.inst >= 0) to_local(sc.inst[ob.inst], lo, ld);
     float t;
+    if constexpr (RTMI_STATS) cnt->flop += 2 * nw_test_flop(ob.aux & 255, false) + 4 + (ob.inst >= 0 ? 15 : 0);
     if (hit_medium(ob, id, lo, ld, d, time, seg_key, t) && !(t < 0.001f)) {
       med_hit |= 1u << m;
       if (t < best_t || (t == best_t && id < best_id)) {
@@ -436,12 +452,20 @@ __device__ __forceinline__ int32_t hit_world_nw(const View &sc, V o, V d, float 
                                        __builtin_fminf(__builtin_fmaxf(tz0, tz1), best_t));
     const bool enter = tnear <= tfar;
     const int32_t leaf = __float_as_int(hi.w);
+    if constexpr (RTMI_STATS) {
+      cnt->flop += 25;
+      cnt->nodes += 1;
+    }
     if (enter && leaf >= 0) {
-      const int32_t first = leaf >> 4, cnt = leaf & 15;
-      for (int32_t k = first; k < first + cnt; ++k) {
+      const int32_t first = leaf >> 4, nleaf = leaf & 15;
+      for (int32_t k = first; k < first + nleaf; ++k) {
         const DevObj ob = objs[k];
         const int twin = ob.ka >> 8;
         if (twin > 0 && ((med_hit >> (twin - 1)) & 1u)) continue;  // hidden by its medium
+        if constexpr (RTMI_STATS) {
+          cnt->flop += nw_test_flop(ob.ka & 255, ob.inst >= 0);
+          cnt->objects += 1;
+        }
         const int32_t id = oids[k];
         float t;
         int face = -1;
@@ -479,7 +503,7 @@ __host__ __device__ constexpr size_t nw_grid_lds_bytes(int32_t nobj, int32_t nce
 // whole shutter (moving spheres) and the composed transform (instances).
 template <bool S = false>
 __device__ __forceinline__ int32_t hit_world_nw_grid(const View &sc, V o, V d, float time, uint64_t seg_key,
-                                                     float &best_t, int &best_face) {
+                                                     float &best_t, int &best_face, NwCount *cnt = nullptr) {
   const DevObj *objs = reinterpret_cast<const DevObj *>(nw_nodes_lds);
   const int32_t *oids = reinterpret_cast<const int32_t *>(nw_nodes_lds + 3 * sc.nobj);
   const uint16_t *cs = reinterpret_cast<const uint16_t *>(oids + sc.nobj);
@@ -500,6 +524,7 @@ __device__ __forceinline__ int32_t hit_world_nw_grid(const View &sc, V o, V d, f
       V lo = o, ld = d;
       if (ob.inst >= 0) to_local(sc.inst[ob.inst], lo, ld);
       float t;
+      if constexpr (RTMI_STATS) cnt->flop += 2 * nw_test_flop(ob.aux & 255, false) + 4 + (ob.inst >= 0 ? 15 : 0);
       if (hit_medium(ob, id, lo, ld, d, time, seg_key, t) && !(t < 0.001f)) {
         med_hit |= 1u << m;
         if (t < best_t || (t == best_t && id < best_id)) {
@@ -514,6 +539,10 @@ __device__ __forceinline__ int32_t hit_world_nw_grid(const View &sc, V o, V d, f
     const DevObj ob = objs[k];
     const int twin = ob.ka >> 8;
     if (!S && twin > 0 && ((med_hit >> (twin - 1)) & 1u)) return;  // hidden by its medium
+    if constexpr (RTMI_STATS) {
+      cnt->flop += nw_test_flop(ob.ka & 255, ob.inst >= 0);
+      cnt->objects += 1;
+    }
     const int32_t id = oids[k];
     float t;
     int face = -1;
@@ -534,6 +563,7 @@ __device__ __forceinline__ int32_t hit_world_nw_grid(const View &sc, V o, V d, f
                                       __builtin_fmaxf(__builtin_fminf(bz0, bz1), 0.0f));
   const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(bx0, bx1), __builtin_fmaxf(by0, by1)),
                                      __builtin_fminf(__builtin_fmaxf(bz0, bz1), best_t));
+  if constexpr (RTMI_STATS) cnt->flop += 25;  // the grid-box clip
   if (tnear <= tfar) {
     auto cell_of = [&](float p, int ax) {
       const int c = int(__builtin_floorf((p - G.g0[ax]) * G.inv_h[ax]));
@@ -550,6 +580,10 @@ __device__ __forceinline__ int32_t hit_world_nw_grid(const View &sc, V o, V d, f
     int cell = cx + G.n[0] * (cy + G.n[1] * cz);
     const int dcx = sx, dcy = sy * G.n[0], dcz = sz * G.n[0] * G.n[1];
     for (;;) {
+      if constexpr (RTMI_STATS) {
+        cnt->flop += 5;
+        cnt->cells += 1;
+      }
       const int e = cs[cell + 1];
       for (int r = cs[cell]; r < e; ++r) test(int32_t(refs[r]));
       const float texit = __builtin_fminf(tnx, __builtin_fminf(tny, tnz));

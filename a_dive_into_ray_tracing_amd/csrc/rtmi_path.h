@@ -401,16 +401,16 @@ static_assert(kLeafMax >= 1 && kLeafMax <= 15, "leaf size");
 // Uniform grid over the small spheres (RT_ACCEL_GRID): cells
 // of size h over the box g0 + [0, n*h) of the spheres' margin-grown boxes.
 // Cell c lists refs[start .. end) (cells[c] = start | end << 16): every
-// sphere whose grown box overlaps it, as 16-bit SCENE indices.  The grid's
-// LDS sphere array holds every sphere of the scene at its scene index (the
-// big spheres' slots unused), so a tie compares scene indices directly and
-// no index table is read.
+// sphere whose grown box overlaps it, as the byte offset (16 x scene index)
+// of its record in the grid's LDS sphere array, which holds every sphere of
+// the scene at its scene index (the big spheres' slots unused): a sphere read
+// is one LDS read at that offset, and a tie compares scene indices directly.
 struct GridDesc {
   float g0[3], h[3], inv_h[3], g1[3];  // origin, cell size, 1/h, far corner
   int32_t n[3];
   int32_t ncells, nrefs;
   const uint32_t *cells;
-  const uint16_t *refs;
+  const uint32_t *refs;
 };
 
 struct Accel {
@@ -450,18 +450,41 @@ __device__ __forceinline__ void stage_bvh(const Accel &g) {
   __syncthreads();
 }
 
+// LDS addresses as 32-bit integers (the offset of a shared variable within
+// the workgroup's LDS) and a float4 read at one: a ds_read_b128 at the value
+// itself.  (Device pass only; the host pass never runs these.)
+__device__ __forceinline__ uint32_t lds_address(const void *p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return uint32_t(size_t((const __attribute__((address_space(3))) char *)p));
+#else
+  return uint32_t(size_t(p));
+#endif
+}
+__device__ __forceinline__ float4 lds_sphere(uint32_t addr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __attribute__((address_space(3))) float4 *p = (const __attribute__((address_space(3))) float4 *)(size_t)addr;
+  return make_float4(p->x, p->y, p->z, p->w);
+#else
+  return make_float4(0.f, 0.f, 0.f, float(addr));
+#endif
+}
+
 // Grid LDS layout: nsph sphere float4s (scene order), ncells uint32 cell
-// ranges, nrefs uint16 references (scenes of < 65536 spheres and refs).
+// ranges, nrefs uint32 references (< 65536 refs).
 __host__ __device__ constexpr size_t grid_lds_bytes(int32_t nsph, int32_t ncells, int32_t nrefs) {
-  return size_t(nsph) * 16 + size_t(ncells) * 4 + (size_t(nrefs) * 2 + 15) / 16 * 16;
+  return size_t(nsph) * 16 + size_t(ncells) * 4 + size_t(nrefs) * 4;
 }
 
 __device__ __forceinline__ void stage_grid(const Accel &g) {
   for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) rtmi_bvh_lds[i] = g.sph[i];
   uint32_t *c = reinterpret_cast<uint32_t *>(rtmi_bvh_lds + g.nsph);
   for (int i = threadIdx.x; i < g.grid.ncells; i += blockDim.x) c[i] = g.grid.cells[i];
-  uint16_t *r = reinterpret_cast<uint16_t *>(c + g.grid.ncells);
-  for (int i = threadIdx.x; i < g.grid.nrefs; i += blockDim.x) r[i] = g.grid.refs[i];
+  // references staged as absolute LDS addresses (the byte offset plus the
+  // sphere array's LDS address): a sphere read is then one ds_read_b128 at
+  // the loaded value, with no address arithmetic
+  uint32_t *r = c + g.grid.ncells;
+  const uint32_t base = lds_address(rtmi_bvh_lds);
+  for (int i = threadIdx.x; i < g.grid.nrefs; i += blockDim.x) r[i] = g.grid.refs[i] + base;
   __syncthreads();
 }
 
@@ -621,9 +644,9 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
   const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(bx0, bx1), __builtin_fmaxf(by0, by1)),
                                      __builtin_fminf(__builtin_fmaxf(bz0, bz1), t_max));
   if (tnear <= tfar) {
-    const float4 *lds_sph = rtmi_bvh_lds;
+    const uint32_t base = lds_address(rtmi_bvh_lds);
     const uint32_t *cells = reinterpret_cast<const uint32_t *>(rtmi_bvh_lds + acc_s.nsph);
-    const uint16_t *refs = reinterpret_cast<const uint16_t *>(cells + G.ncells);
+    const uint32_t *refs = cells + G.ncells;
     // entry cell: the cell of o + tnear*d, clamped into the grid
     auto cell_of = [&](float p, int ax) {
       const int c = int(__builtin_floorf((p - G.g0[ax]) * G.inv_h[ax]));
@@ -649,19 +672,19 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
       if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[2] += 1;
 #endif
       const uint32_t range = cells[cell];
-      for (uint32_t k = range & 0xFFFFu, e = range >> 16; k < e; ++k) {
+      for (const uint32_t *r = refs + (range & 0xFFFFu), *re = refs + (range >> 16); r < re; ++r) {
 #if RTMI_STATS
         gstats[1] += 1;
         if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[3] += 1;
 #endif
-        const int32_t idx = refs[k];
+        const uint32_t addr = *r;
         float hb, disc;
-        sphere_test(lds_sph[idx], d, K, a, aL, mx, my, mz, hb, disc);
+        sphere_test(lds_sphere(addr), d, K, a, aL, mx, my, mz, hb, disc);
         if (!(disc < 0.0f)) {
 #if RTMI_STATS
           if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
 #endif
-          resolve_root(idx, hb, disc, inv_a, t_max, best);
+          resolve_root(int32_t((addr - base) >> 4), hb, disc, inv_a, t_max, best);
         }
       }
       const float texit = __builtin_fminf(tnx, __builtin_fminf(tny, tnz));

@@ -321,9 +321,52 @@ def cpu_baseline():
 
 
 # -------------------------------------------------------------------- main ----
+def nw_executed_counts_child(argv):
+    """--nw-exec-counts child (RTMI_LIBRARY = the RTMI_STATS build): render the
+    given Next-Week rows once and print the executed-work counters."""
+    import ctypes as C
+
+    import torch
+
+    import a_dive_into_ray_tracing_amd as rt
+    import a_dive_into_ray_tracing_amd.nextweek as nw
+
+    which, Wn, Hn, spp, row0, row_step, nrows = (int(x) for x in argv[:7])
+    accel = argv[7]
+    earth = nw.load_image(os.path.join(REPO, "tests", "golden", "earthmap.jpeg")) if which != 1 else None
+    scene, cam = nw.preset(which, image=earth, aspect=Wn / Hn)
+    r = nw.NwRenderer(scene, 0)
+    r.set_accel(accel)
+    L = rt.load()
+    v = (C.c_uint64 * 4)()
+    rt.check(L.rt_nw_debug_counters(v), "rt_nw_debug_counters")  # zero them
+    strip = torch.empty((nrows, Wn, 3), dtype=torch.float32, device="cuda:0")
+    r.render_rows(cam, Wn, Hn, spp, DEPTH, SEED, row0, row_step, nrows, strip.data_ptr(), 0)
+    segs = r.last_segments()
+    rt.check(L.rt_nw_debug_counters(v), "rt_nw_debug_counters")
+    print(json.dumps({"segments": segs, "flop": v[0], "node_visits": v[1], "object_tests": v[2], "cell_steps": v[3]}),
+          flush=True)
+    r.close()
+
+
+def nw_executed_counts(which, Wn, Hn, spp, row0, row_step, nrows, accel):
+    if not os.path.exists(STATS_LIB):
+        return None, f"{STATS_LIB} not built"
+    env = dict(os.environ, RTMI_LIBRARY=STATS_LIB)
+    try:
+        out = subprocess.run([sys.executable, os.path.abspath(__file__), "--nw-exec-counts", str(which), str(Wn), str(Hn),
+                              str(spp), str(row0), str(row_step), str(nrows), accel],
+                             capture_output=True, text=True, timeout=600, env=env, check=True).stdout
+        return json.loads(out.strip().splitlines()[-1]), None
+    except Exception as e:  # reported, never replaced by another figure
+        return None, f"stats child failed: {e}"
+
+
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "--exec-counts":
         return executed_counts_child(sys.argv[2:])
+    if len(sys.argv) > 1 and sys.argv[1] == "--nw-exec-counts":
+        return nw_executed_counts_child(sys.argv[2:])
     if len(sys.argv) > 1 and sys.argv[1] == "--cpu-restatement":
         return cpu_restatement_child(sys.argv[2:])
     ap = argparse.ArgumentParser()
@@ -732,8 +775,16 @@ def bench_nw(args):
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     segs = r.last_segments()
     flop_seg = nw_flop_per_segment(scene.flat())
-    flop_rank = segs * flop_seg  # this rank's launch
-    achieved = flop_rank / (kernel_ms * 1e-3) / 1e12
+    flop_rank = segs * flop_seg  # this rank's launch, brute-force equivalent
+    eq_achieved = flop_rank / (kernel_ms * 1e-3) / 1e12
+    counts, why = None, None
+    if rank == 0 and not args.no_exec_counts:
+        counts, why = nw_executed_counts(which, Wn, Hn, spp, row0, row_step, nrows, args.nw_accel)
+        if counts and counts["segments"] != segs:
+            why, counts = f"stats build segments {counts['segments']} != product {segs}", None
+    elif args.no_exec_counts:
+        why = "skipped (--no-exec-counts)"
+    achieved = counts["flop"] / (kernel_ms * 1e-3) / 1e12 if counts else None
     if rank == 0:
         samples = Wn * Hn * spp
         value = samples * args.steps / elapsed / 1e6
@@ -750,12 +801,20 @@ def bench_nw(args):
                        "accel": accel["accel"], "grid_dims": list(accel["dims"]), "grid_max_cell": accel["max_cell"],
                        "brute_force_objects": accel["n_big"]},
             "roofline": {
-                "bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
-                "flop_per_launch": flop_rank, "flop_per_segment": flop_seg, "segments_per_launch": segs,
-                "kernel_ms": round(kernel_ms, 3), "work_equivalent": True,
-                "note": "brute-force-equivalent FLOP (every object's miss test per world.hit, bench.NW_FLOP) over the "
-                        "BVH / grid kernel's time, as SURVEY 8(d) prescribes for culling: frac can exceed 1",
+                "bound": "valu", "achieved": round(achieved, 3) if achieved else None, "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4) if achieved else None,
+                "traffic": None,
+                "work": "executed: the miss tests the BVH / grid walk performs (bench.NW_FLOP per kind, +15 per "
+                        "instance transform, media 2 x boundary + 4) + 25 per node slab test or grid clip + 5 per "
+                        "cell step, counted per lane by the RTMI_STATS build on the same rows",
+                "flop_per_launch": counts["flop"] if counts else None,
+                "counts": {k: counts[k] for k in ("node_visits", "object_tests", "cell_steps")} if counts else None,
+                "kernel_ms": round(kernel_ms, 3), "segments_per_launch": segs,
+                "work_equivalent_achieved": round(eq_achieved, 3),
+                "work_equivalent_frac": round(eq_achieved / PEAK_FP32_TFLOPS, 4),
+                "work_equivalent_flop_per_segment": flop_seg,
+                "work_equivalent_note": "brute-force-equivalent FLOP (every object's miss test per world.hit) over "
+                                        "the kernel's time, as SURVEY 8(d) prescribes for culling: can exceed 1",
             },
             "kernel_ms": round(kernel_ms, 3),
             "segments_per_sample_rank0": round(segs / (nrows * Wn * spp), 4),
@@ -763,6 +822,8 @@ def bench_nw(args):
             "vs_baseline_ref": "reference rt_next_week CUDA, random_scene with moving spheres 1200x800x500 in 37.88 s "
                                "(RTX 2060 Max-Q): 12.67 Msamples/s",
         }
+        if why:
+            line["roofline"]["note"] = why
         if N == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = nw_cpu_baseline(scene.flat(), cam, which, Wn, Hn)
         print(json.dumps(line), flush=True)

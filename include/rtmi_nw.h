@@ -184,6 +184,12 @@ int rt_nw_ctx_last_kernel(rt_nw_ctx *ctx, int32_t *out4);
  * passes since the last call — closest hit, hit record + texture + scatter,
  * accumulation + regeneration, whole items; RT_EUNSUPPORTED otherwise. */
 int rt_nw_debug_phases(uint64_t *out4);
+/* Analysis: the executed work of the launches since the last call, counted
+ * per lane by the RTMI_STATS build (librtmi_stats.so): {algorithmic FLOP of
+ * the miss tests performed (per-kind counts as bench.py NW_FLOP) + 25 per
+ * node slab test / grid clip + 5 per cell step, node visits, object tests,
+ * cell steps}; zeroed after reading.  RT_EUNSUPPORTED in the product build. */
+int rt_nw_debug_counters(uint64_t *out4);
 
 #ifdef __cplusplus
 }

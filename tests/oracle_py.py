@@ -249,6 +249,21 @@ def nw_math(fn, x):
     return out
 
 
+def nw_box_forms(rays, boxes):
+    """or_nw_box_forms: (t, face) of each ray against its box, division form
+    and reciprocal form."""
+    L = _nw_bind()
+    L.or_nw_box_forms.argtypes = [C.c_int32, _fp, _fp, _fp, _ip, _fp, _ip]
+    rays = np.ascontiguousarray(rays, np.float32)
+    boxes = np.ascontiguousarray(boxes, np.float32)
+    n = rays.shape[0]
+    td, ti = np.zeros(n, np.float32), np.zeros(n, np.float32)
+    fd, fi = np.zeros(n, np.int32), np.zeros(n, np.int32)
+    L.or_nw_box_forms(n, rays.ctypes.data_as(_fp), boxes.ctypes.data_as(_fp), td.ctypes.data_as(_fp),
+                      fd.ctypes.data_as(_ip), ti.ctypes.data_as(_fp), fi.ctypes.data_as(_ip))
+    return td, fd, ti, fi
+
+
 def nw_trace(flat, nwcam, W, H, depth, seed, i, j, smp, cap=64):
     """Oracle mirror of NwRenderer.debug_trace."""
     L = _nw_bind()

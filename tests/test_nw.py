@@ -205,3 +205,30 @@ def test_grid_stats_of_presets():
     s, _ = nw.preset(8, image=np.zeros((4, 4, 3), np.uint8), aspect=1.0)
     g = s.grid_stats()
     assert g["max_cell"] > 24, g
+
+
+def test_reciprocal_plane_form_within_one_ulp_of_reference_division():
+    """The kernels (and the fast oracle) intersect rectangles and box sides
+    with (k - o)*(1/d) instead of aarect.h's (k - o)/d (:41,96,153).  Over
+    random rays against random boxes (and rays aimed at them), the box hit
+    in both forms: the same face except where two faces' parameters lie
+    within an ulp, and t within 1 ulp of the reference's quotient."""
+    rng = np.random.default_rng(7)
+    n = 200_000
+    lo = rng.uniform(-50, 50, (n, 3))
+    hi = lo + rng.uniform(0.01, 20, (n, 3))
+    o = rng.uniform(-80, 80, (n, 3))
+    target = lo + (hi - lo) * rng.uniform(-0.2, 1.2, (n, 3))  # mostly inside, some beside
+    d = (target - o) * rng.uniform(0.1, 10, (n, 1))
+    d[rng.random(n) < 0.05, rng.integers(0, 3)] = 0.0  # axis-parallel rays
+    rays = np.concatenate([o, d], 1)
+    boxes = np.concatenate([lo, hi], 1)
+    td, fd, ti, fi = O.nw_box_forms(rays, boxes)
+    hit = (fd >= 0) & (fi >= 0)
+    assert hit.sum() > n // 2
+    assert ((fd >= 0) != (fi >= 0)).mean() < 1e-3  # hit/miss flips only at an edge, within an ulp
+    same = hit & (fd == fi)
+    assert (hit & (fd != fi)).mean() < 1e-3
+    ulp = np.spacing(np.abs(td[same]).astype(np.float32)).astype(np.float64)
+    dev = np.abs(ti[same].astype(np.float64) - td[same].astype(np.float64)) / ulp
+    assert dev.max() <= 1.0, dev.max()

@@ -1067,7 +1067,7 @@ struct rt_ctx {
   int32_t resident_blocks_bvh = 0;  // persistent grid with the BVH's LDS
   // uniform grid, built by rt_ctx_set_scene beside the BVH
   float4 *grid_sph = nullptr;  // every sphere by scene index
-  uint32_t *grid_cells = nullptr;  // per cell: first | end << 16 into grid_refs
+  uint32_t *grid_cells = nullptr;  // ncells + 1: each cell's first reference
   uint32_t *grid_refs = nullptr;   // 16 x scene index (byte offsets into the LDS sphere array)
   GridDesc grid{};
   int32_t ngrid_sph = 0;
@@ -1339,7 +1339,7 @@ namespace {
 struct GridBuild {
   GridDesc desc{};
   std::vector<float4> sph;     // every sphere of the scene by scene index
-  std::vector<uint32_t> cells;  // per cell: first | end << 16
+  std::vector<uint32_t> cells;  // ncells + 1: each cell's first reference
   std::vector<uint32_t> refs;   // 16 x scene index
 };
 bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, int32_t n, GridBuild &out) {
@@ -1397,13 +1397,12 @@ bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, int32_t 
   }
   // the LDS sphere array: the scene's spheres at their scene indices
   out.sph.assign(b.g.begin(), b.g.begin() + n);
-  out.cells.resize(size_t(total));
+  out.cells.resize(size_t(total) + 1);
   for (int64_t cidx = 0; cidx < total; ++cidx) {
-    const size_t first = out.refs.size();
+    out.cells[size_t(cidx)] = uint32_t(out.refs.size());
     for (uint16_t k : lists[size_t(cidx)]) out.refs.push_back(uint32_t(k) * 16u);
-    if (out.refs.size() > 65535) return false;
-    out.cells[size_t(cidx)] = uint32_t(first) | uint32_t(out.refs.size()) << 16;
   }
+  out.cells[size_t(total)] = uint32_t(out.refs.size());
   out.desc.nrefs = int32_t(out.refs.size());
   return grid_lds_bytes(int32_t(out.sph.size()), out.desc.ncells, out.desc.nrefs) <= kBvhLdsMax;
 }

@@ -400,16 +400,18 @@ static_assert(kLeafMax >= 1 && kLeafMax <= 15, "leaf size");
 
 // Uniform grid over the small spheres (RT_ACCEL_GRID): cells
 // of size h over the box g0 + [0, n*h) of the spheres' margin-grown boxes.
-// Cell c lists refs[start .. end) (cells[c] = start | end << 16): every
-// sphere whose grown box overlaps it, as the byte offset (16 x scene index)
-// of its record in the grid's LDS sphere array, which holds every sphere of
-// the scene at its scene index (the big spheres' slots unused): a sphere read
-// is one LDS read at that offset, and a tie compares scene indices directly.
+// Cell c lists refs[cells[c] .. cells[c+1]): every sphere whose grown box
+// overlaps it, as the byte offset (16 x scene index) of its record in the
+// grid's LDS sphere array, which holds every sphere of the scene at its scene
+// index (the big spheres' slots unused): a tie compares scene indices
+// directly.  In LDS (stage_grid) both arrays hold absolute LDS addresses, so
+// the walk does no address arithmetic: one ds_read2_b32 gives a cell's
+// reference range, one ds_read_b32 a reference, one ds_read_b128 the sphere.
 struct GridDesc {
   float g0[3], h[3], inv_h[3], g1[3];  // origin, cell size, 1/h, far corner
   int32_t n[3];
   int32_t ncells, nrefs;
-  const uint32_t *cells;
+  const uint32_t *cells;  // ncells + 1 first-reference indices
   const uint32_t *refs;
 };
 
@@ -469,23 +471,28 @@ __device__ __forceinline__ float4 lds_sphere(uint32_t addr) {
 #endif
 }
 
-// Grid LDS layout: nsph sphere float4s (scene order), ncells uint32 cell
-// ranges, nrefs uint32 references (< 65536 refs).
+// Grid LDS layout: nsph sphere float4s (scene order), ncells + 1 uint32 cell
+// starts, nrefs uint32 references — all addresses absolute LDS addresses.
 __host__ __device__ constexpr size_t grid_lds_bytes(int32_t nsph, int32_t ncells, int32_t nrefs) {
-  return size_t(nsph) * 16 + size_t(ncells) * 4 + size_t(nrefs) * 4;
+  return size_t(nsph) * 16 + (size_t(ncells) + 1) * 4 + size_t(nrefs) * 4;
 }
 
 __device__ __forceinline__ void stage_grid(const Accel &g) {
   for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) rtmi_bvh_lds[i] = g.sph[i];
   uint32_t *c = reinterpret_cast<uint32_t *>(rtmi_bvh_lds + g.nsph);
-  for (int i = threadIdx.x; i < g.grid.ncells; i += blockDim.x) c[i] = g.grid.cells[i];
-  // references staged as absolute LDS addresses (the byte offset plus the
-  // sphere array's LDS address): a sphere read is then one ds_read_b128 at
-  // the loaded value, with no address arithmetic
-  uint32_t *r = c + g.grid.ncells;
-  const uint32_t base = lds_address(rtmi_bvh_lds);
-  for (int i = threadIdx.x; i < g.grid.nrefs; i += blockDim.x) r[i] = g.grid.refs[i] + base;
+  uint32_t *r = c + g.grid.ncells + 1;
+  const uint32_t sph_base = lds_address(rtmi_bvh_lds), ref_base = lds_address(r);
+  for (int i = threadIdx.x; i <= g.grid.ncells; i += blockDim.x) c[i] = ref_base + 4u * g.grid.cells[i];
+  for (int i = threadIdx.x; i < g.grid.nrefs; i += blockDim.x) r[i] = sph_base + g.grid.refs[i];
   __syncthreads();
+}
+// a uint32 at an LDS address
+__device__ __forceinline__ uint32_t lds_u32(uint32_t addr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return *(const __attribute__((address_space(3))) uint32_t *)(size_t)addr;
+#else
+  return addr;
+#endif
 }
 
 // Inverse direction for culling only (slab tests, grid cell faces): |d_i|
@@ -645,24 +652,36 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
                                      __builtin_fminf(__builtin_fmaxf(bz0, bz1), t_max));
   if (tnear <= tfar) {
     const uint32_t base = lds_address(rtmi_bvh_lds);
-    const uint32_t *cells = reinterpret_cast<const uint32_t *>(rtmi_bvh_lds + acc_s.nsph);
-    const uint32_t *refs = cells + G.ncells;
+    const uint32_t cells = lds_address(rtmi_bvh_lds + acc_s.nsph);  // LDS address of cell 0's start
     // entry cell: the cell of o + tnear*d, clamped into the grid
     auto cell_of = [&](float p, int ax) {
       const int c = int(__builtin_floorf((p - G.g0[ax]) * G.inv_h[ax]));
       return c < 0 ? 0 : (c >= G.n[ax] ? G.n[ax] - 1 : c);
     };
-    int cx = cell_of(__builtin_fmaf(tnear, d.x, o.x), 0);
-    int cy = cell_of(__builtin_fmaf(tnear, d.y, o.y), 1);
-    int cz = cell_of(__builtin_fmaf(tnear, d.z, o.z), 2);
-    const int sx = d.x >= 0.0f ? 1 : -1, sy = d.y >= 0.0f ? 1 : -1, sz = d.z >= 0.0f ? 1 : -1;
-    // parameter of the far face of the current cell on each axis
-    auto tface = [&](int c, int s, int ax, float inv, float oo) {
-      return __builtin_fmaf(__builtin_fmaf(float(c + (s > 0)), G.h[ax], G.g0[ax]), inv, oo);
+    const int cx = cell_of(__builtin_fmaf(tnear, d.x, o.x), 0);
+    const int cy = cell_of(__builtin_fmaf(tnear, d.y, o.y), 1);
+    const int cz = cell_of(__builtin_fmaf(tnear, d.z, o.z), 2);
+    // Per axis: after k steps on it the current cell's far face lies at
+    // t = fma(k, dt, t0) (t0 the entry cell's far face, dt = h/|d_axis|), and
+    // the walk leaves the grid when it would step past kmax.  (Only which
+    // cells are visited depends on these roundings, never a hit: DESIGN.md
+    // §4.5's argument needs face parameters within ~1e-6 of the truth, the
+    // margins being >= 1e-3.)
+    float t0x, t0y, t0z, dtx, dty, dtz, kmx, kmy, kmz;
+    auto axis = [&](float dd, float inv, float oo, int c, int ax, float &t0, float &dt, float &kmax) {
+      const bool pos = dd >= 0.0f;
+      t0 = __builtin_fmaf(__builtin_fmaf(float(c + (pos ? 1 : 0)), G.h[ax], G.g0[ax]), inv, oo);
+      dt = __builtin_fabsf(G.h[ax] * inv);
+      kmax = float(pos ? G.n[ax] - 1 - c : c);
     };
-    float tnx = tface(cx, sx, 0, ix, ox), tny = tface(cy, sy, 1, iy, oy), tnz = tface(cz, sz, 2, iz, oz);
-    int cell = cx + G.n[0] * (cy + G.n[1] * cz);
-    const int dcx = sx, dcy = sy * G.n[0], dcz = sz * G.n[0] * G.n[1];
+    axis(d.x, ix, ox, cx, 0, t0x, dtx, kmx);
+    axis(d.y, iy, oy, cy, 1, t0y, dty, kmy);
+    axis(d.z, iz, oz, cz, 2, t0z, dtz, kmz);
+    float kx = 0.0f, ky = 0.0f, kz = 0.0f, tnx = t0x, tny = t0y, tnz = t0z;
+    // the LDS address of the current cell's start, stepped by 4 x the cell step
+    uint32_t cell = cells + 4u * uint32_t(cx + G.n[0] * (cy + G.n[1] * cz));
+    const int dcx = d.x >= 0.0f ? 4 : -4, dcy = d.y >= 0.0f ? 4 * G.n[0] : -4 * G.n[0];
+    const int dcz = d.z >= 0.0f ? 4 * G.n[0] * G.n[1] : -4 * G.n[0] * G.n[1];
 #if RTMI_TRACE_PHASES
     tp2 = __builtin_amdgcn_s_memtime();
 #endif
@@ -671,13 +690,13 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
       gstats[0] += 1;
       if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[2] += 1;
 #endif
-      const uint32_t range = cells[cell];
-      for (const uint32_t *r = refs + (range & 0xFFFFu), *re = refs + (range >> 16); r < re; ++r) {
+      const uint32_t re = lds_u32(cell + 4u);  // (with the next one: a ds_read2_b32)
+      for (uint32_t r = lds_u32(cell); r < re; r += 4u) {
 #if RTMI_STATS
         gstats[1] += 1;
         if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[3] += 1;
 #endif
-        const uint32_t addr = *r;
+        const uint32_t addr = lds_u32(r);
         float hb, disc;
         sphere_test(lds_sphere(addr), d, K, a, aL, mx, my, mz, hb, disc);
         if (!(disc < 0.0f)) {
@@ -690,20 +709,20 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
       const float texit = __builtin_fminf(tnx, __builtin_fminf(tny, tnz));
       if (!(texit < t_max)) break;  // the closest hit so far lies in the cells walked
       if (tnx <= tny && tnx <= tnz) {
-        cx += sx;
-        if (unsigned(cx) >= unsigned(G.n[0])) break;
+        if (kx >= kmx) break;  // leaves the grid
+        kx += 1.0f;
+        tnx = __builtin_fmaf(kx, dtx, t0x);
         cell += dcx;
-        tnx = tface(cx, sx, 0, ix, ox);
       } else if (tny <= tnz) {
-        cy += sy;
-        if (unsigned(cy) >= unsigned(G.n[1])) break;
+        if (ky >= kmy) break;
+        ky += 1.0f;
+        tny = __builtin_fmaf(ky, dty, t0y);
         cell += dcy;
-        tny = tface(cy, sy, 1, iy, oy);
       } else {
-        cz += sz;
-        if (unsigned(cz) >= unsigned(G.n[2])) break;
+        if (kz >= kmz) break;
+        kz += 1.0f;
+        tnz = __builtin_fmaf(kz, dtz, t0z);
         cell += dcz;
-        tnz = tface(cz, sz, 2, iz, oz);
       }
     }
   }

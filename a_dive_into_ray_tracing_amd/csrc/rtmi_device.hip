@@ -82,7 +82,21 @@ struct RenderArgs {
   // and per-tile world.hit counts of this launch (null: not measured)
   const int32_t *tile_order;
   unsigned *tile_cost;
+  // hand-off of an item's last paths (chunked grid-kernel
+  // launches): once all of an item's jobs are taken and at most
+  // handoff_lanes of its paths are live, they are written to the hand-off
+  // buffer (kHandoffFields arrays of handoff_cap, structure of arrays) and the
+  // wave leaves; handoff_kernel finishes them.  null: off.
+  float *handoff;
+  unsigned *handoff_count;  // slots reserved (may exceed the capacity: those paths stayed)
+  uint32_t handoff_cap;
+  int32_t handoff_lanes;
 };
+// a handed-off path: o, d, T (9 floats), the generator (4 words), depth,
+// pixel (row-major index into the launch's W x rows strip; ~0u: an empty
+// slot), and one spare field
+constexpr int kHandoffFields = 16;
+constexpr uint32_t kHandoffEmpty = 0xFFFFFFFFu;
 
 #ifndef RTMI_WAVES_PER_BLOCK
 #define RTMI_WAVES_PER_BLOCK 4
@@ -102,11 +116,10 @@ __device__ unsigned long long g_trace[kTraceCap * 4];
 __device__ unsigned g_trace_n;
 #define RTMI_TRACE_BEGIN                                                                 \
   const unsigned long long trace_t0 = __builtin_amdgcn_s_memrealtime();                  \
-  const unsigned long long cyc_start = __builtin_amdgcn_s_memtime();                     \
-  unsigned long long cyc_hit = 0;
+  const unsigned long long cyc_start = __builtin_amdgcn_s_memtime();
 #define RTMI_TRACE_END(items)                                                            \
   if (lane == 0) {                                                                       \
-    atomicAdd(&segments[5], cyc_hit);                                                    \
+    atomicAdd(&segments[5], cnt.cyc_hit);                                                \
     atomicAdd(&segments[6], __builtin_amdgcn_s_memtime() - cyc_start);                   \
     const unsigned k_ = atomicAdd(&g_trace_n, 1u);                                       \
     if (k_ < kTraceCap) {                                                                \
@@ -123,32 +136,10 @@ __device__ unsigned g_trace_n;
 #define RTMI_TRACE_END(items)
 #endif
 
-#ifndef RTMI_FAIR
-#define RTMI_FAIR 3
-#endif
-// the grid kernel keeps the camera in LDS (config 2: 30.1 -> 28.2 ms: the
-// scalar registers it occupied were spilled to VGPR lanes and read back
-// with v_readlane at every regeneration)
-#ifndef RTMI_CAM_LDS
-#define RTMI_CAM_LDS 1
-#endif
-// Fast mode: u, v = (i + ju) * (1/(W-1)), (j + jv) * (1/(H-1)) — the
-// reciprocals once per block instead of two divisions per camera ray (<= 1
-// ulp from main.cpp:278-279's quotients; the oracle's fast mode computes the
-// same products).  0: the quotients (A/B only; the oracle does not follow).
-#ifndef RTMI_UV_RCP
-#define RTMI_UV_RCP 1
-#endif
-#ifndef RTMI_REGEN_TWICE
-#define RTMI_REGEN_TWICE 0
-#endif
 // RTMI_CHECK builds (analysis only) bounds-check every accumulator write and
 // count violations in segments[5..7] instead of performing them.
 #ifndef RTMI_CHECK
 #define RTMI_CHECK 0
-#endif
-#ifndef RTMI_FAIR_TIME
-#define RTMI_FAIR_TIME 0
 #endif
 #ifndef RTMI_PERSIST_MIN_BLOCKS
 #define RTMI_PERSIST_MIN_BLOCKS 1
@@ -213,9 +204,13 @@ template <int ACC> struct PersistShape {
   static constexpr int per_eu = ACC ? RTMI_PERSIST_ACC_PER_EU : RTMI_PERSIST_MIN_BLOCKS;
 };
 
-#if RTMI_CAM_LDS
-// The camera and the (W-1, H-1) denominators of main.cpp:278-279 in LDS
-// (21 floats), read at each regeneration instead of held in scalar registers.
+// The camera and the reciprocals of main.cpp:278-279's (W-1, H-1)
+// denominators in LDS (21 floats), read at each regeneration instead of held
+// in scalar registers (config 2: 30.1 -> 28.2 ms: the scalar registers the
+// camera occupied were spilled to VGPR lanes and read back with v_readlane).
+// Fast mode: u, v = (i + ju) * (1/(W-1)), (j + jv) * (1/(H-1)) — <= 1 ulp from
+// the reference's quotients, two divisions fewer per camera ray (the
+// oracle's fast mode computes the same products).
 __device__ __forceinline__ void stage_camera(float *cam_lds, const RenderArgs &a) {
   const unsigned t = threadIdx.x;
   if (t < 19) {
@@ -231,11 +226,7 @@ __device__ __forceinline__ void stage_camera(float *cam_lds, const RenderArgs &a
     }
     cam_lds[t] = v;
   } else if (t < 21) {
-#if RTMI_UV_RCP
     cam_lds[t] = 1.0f / float((t == 19 ? a.W : a.H) - 1);
-#else
-    cam_lds[t] = float((t == 19 ? a.W : a.H) - 1);
-#endif
   }
 }
 __device__ __forceinline__ Cam<float> lds_camera(const float *cam_lds) {
@@ -249,7 +240,124 @@ __device__ __forceinline__ Cam<float> lds_camera(const float *cam_lds) {
   cm.lens = cam_lds[18];
   return cm;
 }
+// Per-lane work counters of the analysis builds (RTMI_STATS: the executed
+// work; RTMI_TRACE_PHASES / RTMI_TRACE: cycle clocks); empty in the product.
+struct SegCounters {
+#if RTMI_STATS
+  unsigned stats[4];      // brute force: groups, groups with a candidate (wave), resolves (lane), sphere resolves (wave)
+  unsigned bvh_stats[5];  // BVH / grid: node (cell) visits, leaf (cell) sphere tests (lane); node iterations,
+                          // leaf-sphere iterations, root resolutions (wave)
 #endif
+#if RTMI_TRACE_PHASES
+  PhaseClock pc;
+#endif
+#if RTMI_TRACE
+  unsigned long long cyc_hit;
+#endif
+};
+
+__device__ __forceinline__ void flush_counters(const SegCounters &cnt, int lane, unsigned long long *segments) {
+#if RTMI_STATS
+  // brute force: [1] groups, [2] groups with a candidate, [4] sphere
+  // resolves (wave); BVH / grid: [1] node iterations, [2] leaf-sphere
+  // iterations, [4] root resolutions (wave).  [3] resolves (lane), [5] node
+  // visits, [6] leaf sphere tests (lane).
+  if (lane == 0) {
+    atomicAdd(&segments[1], (unsigned long long)cnt.stats[0]);
+    atomicAdd(&segments[2], (unsigned long long)cnt.stats[1]);
+    atomicAdd(&segments[4], (unsigned long long)cnt.stats[3]);
+  }
+  atomicAdd(&segments[3], (unsigned long long)cnt.stats[2]);
+  atomicAdd(&segments[5], (unsigned long long)cnt.bvh_stats[0]);
+  atomicAdd(&segments[6], (unsigned long long)cnt.bvh_stats[1]);
+  atomicAdd(&segments[1], (unsigned long long)cnt.bvh_stats[2]);
+  atomicAdd(&segments[2], (unsigned long long)cnt.bvh_stats[3]);
+  atomicAdd(&segments[4], (unsigned long long)cnt.bvh_stats[4]);
+#else
+  (void)cnt, (void)lane, (void)segments;
+#endif
+}
+
+// One segment of a path — the body of the reference's recursive ray_color
+// (main.cpp:57-83) as one step of an iterative loop: the closest hit (brute
+// force, BVH or grid: the same hit bit for bit), then the sky of a miss,
+// absorption, or the scattered ray with its robustness offset.  Returns true
+// when the path ended: col is then its colour (black when absorbed or out of
+// depth).  Shared by every fast kernel, so they compute identical paths.
+template <int ACC>
+__device__ __forceinline__ bool path_segment(const SceneView<float> &sc, const SpherePair *__restrict__ pairs,
+                                             const RenderArgs &a, V3<float> &o, V3<float> &d, V3<float> &T,
+                                             int &depth, Xoro &rng, V3<float> &col, SegCounters &cnt,
+                                             unsigned long long *segments) {
+  (void)cnt, (void)segments;
+  float t;
+#if RTMI_TRACE
+  const unsigned long long cyc0 = __builtin_amdgcn_s_memtime();
+#endif
+  int k;
+  if constexpr (ACC == 1) {
+    k = hit_world_bvh<kBigGroup>(a.acc, o, d, t
+#if RTMI_STATS
+                                  , cnt.bvh_stats
+#endif
+    );
+  } else if constexpr (ACC == 2) {
+    k = hit_world_grid<kBigGroup>(a.acc, o, d, t
+#if RTMI_STATS
+                                   , cnt.bvh_stats
+#endif
+#if RTMI_TRACE_PHASES
+                                   , cnt.pc
+#endif
+    );
+  } else {
+    k = hit_world_packed<kPairGroup>(pairs, a.npairs, o, d, t
+#if RTMI_STATS
+                                     , cnt.stats
+#endif
+    );
+  }
+#if RTMI_TRACE
+  cnt.cyc_hit += __builtin_amdgcn_s_memtime() - cyc0;
+#endif
+#if RTMI_CHECK
+  if (k >= a.n) atomicAdd(&segments[7], 1ull << 32);
+#endif
+  // 1/|d| once for the lanes that need it: the sky of a miss (main.cpp:80)
+  // and unit(din) of metal and dielectric — the same expression
+  const bool miss = k < 0 || (RTMI_CHECK && k >= a.n);
+  // the hit sphere's three records in one memory round trip (a miss reads
+  // sphere 0's, unused)
+  const int kk = miss ? 0 : k;
+  const float4 sh1k = sc.sh1[kk], sh0k = sc.sh0[kk], geomk = sc.geom[kk];
+  const int kind = miss ? -1 : int(sh1k.x);
+  float inv_len = 0.0f;
+  if (kind != RT_MAT_LAMBERTIAN) inv_len = 1.0f / dsqrt(dot<true>(d, d));
+  if (miss) {
+    const V3<float> sk = sky_fast(d, inv_len);
+    col = mk(T.x * sk.x, T.y * sk.y, T.z * sk.z);
+    return true;
+  }
+  V3<float> p, nrm, at, nd;
+  bool front;
+  hit_record_fast(geomk, sh0k.x, o, d, t, p, nrm, front);
+  if (!scatter_fast(sh0k, sh1k, d, nrm, front, rng, at, nd, inv_len))
+    return true;  // absorbed (metal below the surface): black, main.cpp:78
+  T = mk(T.x * at.x, T.y * at.y, T.z * at.z);
+  // float robustness: start the next segment
+  // 2^-14 * (1 + |p|_inf) off the surface, on the side the scattered ray
+  // leaves on, so float hit-point error (~1e-6) cannot re-hit the surface
+  // just left or trap the path inside an opaque sphere.
+  float m = __builtin_fabsf(p.x);
+  if (__builtin_fabsf(p.y) > m) m = __builtin_fabsf(p.y);
+  if (__builtin_fabsf(p.z) > m) m = __builtin_fabsf(p.z);
+  float delta = 0x1p-14f * (1.0f + m);
+  if (dot<true>(nd, nrm) < 0.f) delta = -delta;
+  o = mk(__builtin_fmaf(delta, nrm.x, p.x), __builtin_fmaf(delta, nrm.y, p.y), __builtin_fmaf(delta, nrm.z, p.z));
+  d = nd;
+  return ++depth >= a.max_depth;  // depth exhausted: black, main.cpp:58-60
+}
+
 // ACC: 0 brute force, 1 BVH, 2 uniform grid (RT_ACCEL_*); the accelerated
 // kernels stage their structure in LDS and share the block shape.
 template <int TW, bool CHUNKED, int ACC>
@@ -262,35 +370,14 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   __shared__ unsigned long long acc[WPB][3][64];
   __shared__ unsigned long long wave_segs[WPB];
   __shared__ unsigned pool_next;  // block pool: next unclaimed job
-#if RTMI_CAM_LDS
-  // the camera in LDS, read at each regeneration: kept out of the wave's
-  // scalar registers (which spill it to VGPR lanes otherwise)
-  __shared__ float cam_lds[21];
-#endif
+  __shared__ float cam_lds[21];  // the camera (stage_camera)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * WPB + wave;
   const bool pool = CHUNKED && a.block_pool;  // block-uniform (implies block_flush)
   if (pool && threadIdx.x == 0) pool_next = 64 * WPB;
-#if RTMI_CAM_LDS
-  if (threadIdx.x < 19) {
-    float v;
-    switch (threadIdx.x / 3) {
-      case 0: v = (&a.cam.origin.x)[threadIdx.x % 3]; break;
-      case 1: v = (&a.cam.llc.x)[threadIdx.x % 3]; break;
-      case 2: v = (&a.cam.hor.x)[threadIdx.x % 3]; break;
-      case 3: v = (&a.cam.ver.x)[threadIdx.x % 3]; break;
-      case 4: v = (&a.cam.u.x)[threadIdx.x % 3]; break;
-      case 5: v = (&a.cam.v.x)[threadIdx.x % 3]; break;
-      default: v = a.cam.lens; break;
-    }
-    cam_lds[threadIdx.x] = v;
-  }
-#if RTMI_UV_RCP
-  else if (threadIdx.x < 21) cam_lds[threadIdx.x] = 1.0f / float((threadIdx.x == 19 ? a.W : a.H) - 1);
-#endif
+  stage_camera(cam_lds, a);
   if constexpr (ACC == 0) __syncthreads();  // (accelerated kernels: stage_* ends with one)
-#endif
   if constexpr (ACC == 1) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
   else if constexpr (ACC == 2) stage_grid(a.acc);
   else if (pool) __syncthreads();
@@ -330,13 +417,9 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   if (lane == 0) wave_segs[wave] = 0;
   unsigned nseg = 0;  // world.hit calls of this lane (algorithmic-work accounting)
   RTMI_TRACE_BEGIN
+  SegCounters cnt{};
 #if RTMI_TRACE_PHASES
-  PhaseClock phase_clock{{0, 0, 0}};
   unsigned long long cyc_iter = 0, cyc_regen = 0, cyc_ramp = 0;
-#endif
-#if RTMI_STATS
-  unsigned stats[4] = {0, 0, 0, 0};  // groups, groups with a candidate (wave), resolves (lane), sphere resolves (wave)
-  unsigned bvh_stats[5] = {0, 0, 0, 0, 0};  // BVH: node visits, leaf sphere tests (lane); node iterations, leaf-sphere iterations, root resolutions (wave)
 #endif
 
   const SceneView<float> sc{geom, sh0, sh1, a.n};
@@ -360,28 +443,10 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
     rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(a.s_base + s));
     float ju, jv;
     rng.pair(ju, jv);
-#if RTMI_UV_RCP
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // camera read here, not hoisted out of the loop
     const float u = (float(i) + ju) * cam_lds[19];  // main.cpp:278, by the reciprocal
     const float v = (float(j) + jv) * cam_lds[20];  // main.cpp:279
-#else
-    const float u = (float(i) + ju) / float(a.W - 1);  // main.cpp:278
-    const float v = (float(j) + jv) / float(a.H - 1);  // main.cpp:279
-#endif
-#if RTMI_CAM_LDS
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // read here, not hoisted out of the loop
-    Cam<float> cm;
-    cm.origin = mk(cam_lds[0], cam_lds[1], cam_lds[2]);
-    cm.llc = mk(cam_lds[3], cam_lds[4], cam_lds[5]);
-    cm.hor = mk(cam_lds[6], cam_lds[7], cam_lds[8]);
-    cm.ver = mk(cam_lds[9], cam_lds[10], cam_lds[11]);
-    cm.u = mk(cam_lds[12], cam_lds[13], cam_lds[14]);
-    cm.v = mk(cam_lds[15], cam_lds[16], cam_lds[17]);
-    cm.lens = cam_lds[18];
-    get_ray<true, float>(cm, u, v, rng, o, d);
-#else
-    get_ray<true, float>(a.cam, u, v, rng, o, d);
-#endif
+    get_ray<true, float>(lds_camera(cam_lds), u, v, rng, o, d);
     T = mk(1.f, 1.f, 1.f);
     depth = 0;
   };
@@ -398,76 +463,8 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
     const unsigned long long cyc_a = __builtin_amdgcn_s_memtime();
 #endif
     if (active) {
-      float t;
       ++nseg;
-#if RTMI_TRACE
-      const unsigned long long cyc0 = __builtin_amdgcn_s_memtime();
-#endif
-      int k;
-      if constexpr (ACC == 1) {
-        k = hit_world_bvh<kBigGroup>(a.acc, o, d, t
-#if RTMI_STATS
-                                      , bvh_stats
-#endif
-        );
-      } else if constexpr (ACC == 2) {
-        k = hit_world_grid<kBigGroup>(a.acc, o, d, t
-#if RTMI_STATS
-                                       , bvh_stats
-#endif
-#if RTMI_TRACE_PHASES
-                                       , phase_clock
-#endif
-        );
-      } else {
-        k = hit_world_packed<kPairGroup>(pairs, a.npairs, o, d, t
-#if RTMI_STATS
-                                         , stats
-#endif
-        );
-      }
-#if RTMI_TRACE
-      cyc_hit += __builtin_amdgcn_s_memtime() - cyc0;
-#endif
-#if RTMI_CHECK
-      if (k >= a.n) atomicAdd(&segments[7], 1ull << 32);
-#endif
-      // 1/|d| once for the lanes that need it: the sky of a miss (main.cpp:80)
-      // and unit(din) of metal and dielectric — the same expression
-      const bool miss = k < 0 || (RTMI_CHECK && k >= a.n);
-      // the hit sphere's three records in one memory round trip (a miss reads
-      // sphere 0's, unused)
-      const int kk = miss ? 0 : k;
-      const float4 sh1k = sc.sh1[kk], sh0k = sc.sh0[kk], geomk = sc.geom[kk];
-      const int kind = miss ? -1 : int(sh1k.x);
-      float inv_len = 0.0f;
-      if (kind != RT_MAT_LAMBERTIAN) inv_len = 1.0f / dsqrt(dot<true>(d, d));
-      if (miss) {
-        const V3<float> sk = sky_fast(d, inv_len);
-        col = mk(T.x * sk.x, T.y * sk.y, T.z * sk.z);
-        done = true;
-      } else {
-        V3<float> p, nrm, at, nd;
-        bool front;
-        hit_record_fast(geomk, sh0k.x, o, d, t, p, nrm, front);
-        if (!scatter_fast(sh0k, sh1k, d, nrm, front, rng, at, nd, inv_len)) {
-          done = true;  // absorbed (metal below the surface): black, main.cpp:78
-        } else {
-          T = mk(T.x * at.x, T.y * at.y, T.z * at.z);
-          // float robustness: start the next segment
-          // 2^-14 * (1 + |p|_inf) off the surface, on the side the scattered
-          // ray leaves on, so float hit-point error (~1e-6) cannot re-hit the
-          // surface just left or trap the path inside an opaque sphere.
-          float m = __builtin_fabsf(p.x);
-          if (__builtin_fabsf(p.y) > m) m = __builtin_fabsf(p.y);
-          if (__builtin_fabsf(p.z) > m) m = __builtin_fabsf(p.z);
-          float delta = 0x1p-14f * (1.0f + m);
-          if (dot<true>(nd, nrm) < 0.f) delta = -delta;
-          o = mk(__builtin_fmaf(delta, nrm.x, p.x), __builtin_fmaf(delta, nrm.y, p.y), __builtin_fmaf(delta, nrm.z, p.z));
-          d = nd;
-          if (++depth >= a.max_depth) done = true;  // depth exhausted: black, main.cpp:58-60
-        }
-      }
+      done = path_segment<ACC>(sc, pairs, a, o, d, T, depth, rng, col, cnt, segments);
     }
 #if RTMI_TRACE_PHASES
     const unsigned long long cyc_b = __builtin_amdgcn_s_memtime();
@@ -487,15 +484,47 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
         atomicAdd(&acc[wave][2][px], (unsigned long long)to_fixed(col.z));
         const int rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
         const int q = next + rank;
-#if RTMI_REGEN_TWICE
-        // analysis only: the regeneration executed twice (same result) to
-        // measure its marginal cost
-        if (q < nq) { int q2 = q; asm volatile("" : "+v"(q2)); start(q2); asm volatile("" : "+v"(px)); }
-#endif
         if (q < nq) start(q);
         else active = false;
       }
       next += __popcll(m);
+    }
+    if constexpr (CHUNKED) {
+      // ramp-down hand-off: all jobs taken (wave-uniform),
+      // few paths live -> write them out and leave
+      if (a.handoff && !pool && next >= nq) {
+        const unsigned long long live = __ballot(active);
+        const int n = __popcll(live);
+        if (n > 0 && n <= a.handoff_lanes) {
+          unsigned base = 0;
+          if (lane == 0) base = atomicAdd(a.handoff_count, unsigned(n));
+          base = __builtin_amdgcn_readfirstlane(base);
+          const bool fits = uint64_t(base) + uint64_t(n) <= uint64_t(a.handoff_cap);  // wave-uniform
+          if (active) {
+            const unsigned slot = base + __builtin_amdgcn_mbcnt_hi(unsigned(live >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo(unsigned(live), 0u));
+            if (slot < a.handoff_cap) {  // a reserved slot below the capacity is always written
+              float *h = a.handoff + slot;
+              const size_t cap = a.handoff_cap;
+              uint32_t pix = kHandoffEmpty;
+              if (fits) {
+                const int ly = div_small(px, vw, inv_vw), lx = px - ly * vw;
+                pix = uint32_t(y0 + ly) * uint32_t(a.W) + uint32_t(x0 + lx);
+                h[0 * cap] = o.x; h[1 * cap] = o.y; h[2 * cap] = o.z;
+                h[3 * cap] = d.x; h[4 * cap] = d.y; h[5 * cap] = d.z;
+                h[6 * cap] = T.x; h[7 * cap] = T.y; h[8 * cap] = T.z;
+                h[9 * cap] = __uint_as_float(uint32_t(rng.s0));
+                h[10 * cap] = __uint_as_float(uint32_t(rng.s0 >> 32));
+                h[11 * cap] = __uint_as_float(uint32_t(rng.s1));
+                h[12 * cap] = __uint_as_float(uint32_t(rng.s1 >> 32));
+                h[13 * cap] = __int_as_float(depth);
+              }
+              h[14 * cap] = __uint_as_float(pix);
+            }
+          }
+          if (fits) active = false;  // (else: the buffer is full, the wave finishes its paths)
+        }
+      }
     }
 #if RTMI_TRACE_PHASES
     const unsigned long long cyc_e = __builtin_amdgcn_s_memtime();
@@ -511,25 +540,13 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
     atomicAdd(segments, wave_segs[wave]);
     if (a.tile_cost) atomicAdd(&a.tile_cost[tile], unsigned(wave_segs[wave]));
   }
-#if RTMI_STATS
-  // brute force: [1] groups, [2] groups with a candidate, [4] sphere
-  // resolves (wave); BVH: [1] node iterations, [2] leaf-sphere iterations,
-  // [4] root resolutions (wave).  [3] resolves (lane), [5] node visits,
-  // [6] leaf sphere tests (lane).
-  if (lane == 0) { atomicAdd(&segments[1], (unsigned long long)stats[0]); atomicAdd(&segments[2], (unsigned long long)stats[1]); atomicAdd(&segments[4], (unsigned long long)stats[3]); }
-  atomicAdd(&segments[3], (unsigned long long)stats[2]);
-  atomicAdd(&segments[5], (unsigned long long)bvh_stats[0]);
-  atomicAdd(&segments[6], (unsigned long long)bvh_stats[1]);
-  atomicAdd(&segments[1], (unsigned long long)bvh_stats[2]);
-  atomicAdd(&segments[2], (unsigned long long)bvh_stats[3]);
-  atomicAdd(&segments[4], (unsigned long long)bvh_stats[4]);
-#endif
+  flush_counters(cnt, lane, segments);
 #if RTMI_TRACE_PHASES
   // [1] big spheres + clip/setup, [2] loop passes after the item's last job
   // was taken (ramp-down), [3] cell walk
-  phase_clock.c[0] += phase_clock.c[1];
-  phase_clock.c[1] = cyc_ramp;
-  if (lane == 0) for (int q = 0; q < 3; ++q) atomicAdd(&segments[1 + q], phase_clock.c[q]);
+  cnt.pc.c[0] += cnt.pc.c[1];
+  cnt.pc.c[1] = cyc_ramp;
+  if (lane == 0) for (int q = 0; q < 3; ++q) atomicAdd(&segments[1 + q], cnt.pc.c[q]);
   // wave-level: [4] hit + shading passes, [7] accumulation + regeneration
   if (lane == 0) { atomicAdd(&segments[4], cyc_iter); atomicAdd(&segments[7], cyc_regen); }
 #endif
@@ -566,6 +583,89 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
       else out[o3 + c] = from_fixed((long long)v);
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// hand-off kernel: finishes the paths render_kernel handed off
+// ---------------------------------------------------------------------------
+// Each wave takes kHandoffPerWave consecutive slots of the hand-off buffer as
+// its job queue: a lane whose path ends adds its colour to the fixed-point
+// accumulator (global int64 atomics: the sums are order-independent, so the
+// image is the same bit for bit) and loads the next slot (the main kernel's
+// ballot + mbcnt regeneration), so lanes stay busy until the queue's last
+// paths.  Empty slots (kHandoffEmpty) are skipped.
+constexpr int kHandoffPerWave = 256;
+constexpr int kHandoffWaves = 4;  // waves per block
+
+template <int ACC>
+__global__ __launch_bounds__(64 * kHandoffWaves) void handoff_kernel(
+    const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1,
+    const SpherePair *__restrict__ pairs, RenderArgs a, unsigned long long *__restrict__ accum,
+    unsigned long long *__restrict__ segments) {
+  if constexpr (ACC == 1) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
+  else if constexpr (ACC == 2) stage_grid(a.acc);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const unsigned total = min(*a.handoff_count, a.handoff_cap);
+  const unsigned q_base = (unsigned(blockIdx.x) * kHandoffWaves + unsigned(wave)) * unsigned(kHandoffPerWave);
+  if (q_base >= total) return;  // wave-uniform
+  const int nq = int(min(total - q_base, unsigned(kHandoffPerWave)));
+  const SceneView<float> sc{geom, sh0, sh1, a.n};
+  const size_t cap = a.handoff_cap;
+  SegCounters cnt{};
+  unsigned nseg = 0;
+  V3<float> o, d, T;
+  int depth = 0;
+  uint32_t pix = kHandoffEmpty;
+  Xoro rng;
+  auto load = [&](int q) {
+    const float *h = a.handoff + q_base + unsigned(q);
+    o = mk(h[0 * cap], h[1 * cap], h[2 * cap]);
+    d = mk(h[3 * cap], h[4 * cap], h[5 * cap]);
+    T = mk(h[6 * cap], h[7 * cap], h[8 * cap]);
+    rng.s0 = uint64_t(__float_as_uint(h[9 * cap])) | uint64_t(__float_as_uint(h[10 * cap])) << 32;
+    rng.s1 = uint64_t(__float_as_uint(h[11 * cap])) | uint64_t(__float_as_uint(h[12 * cap])) << 32;
+    depth = __float_as_int(h[13 * cap]);
+    pix = __float_as_uint(h[14 * cap]);
+    // a pixel outside the launch's strip (never written so) is an empty slot
+    if (uint64_t(pix) * 3 >= a.out_elems) pix = kHandoffEmpty;
+  };
+  bool active = lane < nq;
+  if (active) load(lane);
+  int next = 64;
+  for (;;) {
+    if (__ballot(active) == 0) break;
+    bool done = false;
+    V3<float> col = mk(0.f, 0.f, 0.f);
+    if (active) {
+      if (pix == kHandoffEmpty) {
+        done = true;
+      } else {
+        ++nseg;
+        done = path_segment<ACC>(sc, pairs, a, o, d, T, depth, rng, col, cnt, segments);
+      }
+    }
+    const unsigned long long m = __ballot(done);
+    if (m) {
+      if (done) {
+        if (pix != kHandoffEmpty) {
+          unsigned long long *acc3 = accum + size_t(pix) * 3;
+          atomicAdd(&acc3[0], (unsigned long long)to_fixed(col.x));
+          atomicAdd(&acc3[1], (unsigned long long)to_fixed(col.y));
+          atomicAdd(&acc3[2], (unsigned long long)to_fixed(col.z));
+        }
+        const int q = next + __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
+        if (q < nq) load(q);
+        else active = false;
+      }
+      next += __popcll(m);
+    }
+  }
+  // world.hit calls: one atomic per wave
+  unsigned long long ws = nseg;
+  for (int off = 32; off > 0; off >>= 1) ws += __shfl_xor(ws, off);
+  if (lane == 0) atomicAdd(segments, ws);
+  flush_counters(cnt, lane, segments);
 }
 
 // ---------------------------------------------------------------------------
@@ -626,11 +726,9 @@ __global__ __launch_bounds__(64 * PersistShape<ACC>::waves, PersistShape<ACC>::p
   __shared__ int item_lds[WPB][2][8];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-#if RTMI_CAM_LDS
   __shared__ float cam_lds[21];
   stage_camera(cam_lds, a);
   if constexpr (ACC == 0) __syncthreads();  // (accelerated kernels: stage_* ends with one)
-#endif
   if constexpr (ACC == 1) stage_bvh(a.acc);
   else if constexpr (ACC == 2) stage_grid(a.acc);
   if (lane < 2) slot_segs[wave][lane] = 0;
@@ -640,26 +738,11 @@ __global__ __launch_bounds__(64 * PersistShape<ACC>::waves, PersistShape<ACC>::p
   unsigned nseg = 0;
   int n_taken = 0;
   RTMI_TRACE_BEGIN
-#if RTMI_TRACE_PHASES
-  PhaseClock phase_clock{{0, 0, 0}};
-#endif
-#if RTMI_STATS
-  unsigned stats[4] = {0, 0, 0, 0};
-  unsigned bvh_stats[5] = {0, 0, 0, 0, 0};
-#endif
+  SegCounters cnt{};
   const SceneView<float> sc{geom, sh0, sh1, a.n};
 
-#if RTMI_FAIR == 2
-  {  // experiment: priority by hardware wave slot (inverts the age order)
-    const unsigned slot = __builtin_amdgcn_s_getreg(0xF804) & 15u;
-    if (slot >= 3) __builtin_amdgcn_s_setprio(3);
-    else if (slot == 2) __builtin_amdgcn_s_setprio(2);
-    else if (slot == 1) __builtin_amdgcn_s_setprio(1);
-  }
-#endif
-#if RTMI_FAIR == 3
-  unsigned prio_phase = __builtin_amdgcn_s_getreg(0xF804) & 15u;  // hardware wave slot
-#endif
+  // issue-priority rotation, starting at the hardware wave slot
+  unsigned prio_phase = __builtin_amdgcn_s_getreg(0xF804) & 15u;
   // wave-uniform slot state: the current item (slot `cur`) hands out jobs;
   // the previous one (slot cur^1, all jobs handed out) may still have paths
   // in flight.
@@ -721,20 +804,9 @@ __global__ __launch_bounds__(64 * PersistShape<ACC>::waves, PersistShape<ACC>::p
           rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(it[4] + qs));
           float ju, jv;
           rng.pair(ju, jv);
-#if RTMI_CAM_LDS
-#if RTMI_UV_RCP
           const float u = (float(i) + ju) * cam_lds[19];  // main.cpp:278, by the reciprocal
           const float v = (float(j) + jv) * cam_lds[20];  // main.cpp:279
-#else
-          const float u = (float(i) + ju) / cam_lds[19];  // main.cpp:278
-          const float v = (float(j) + jv) / cam_lds[20];  // main.cpp:279
-#endif
           get_ray<true, float>(lds_camera(cam_lds), u, v, rng, o, d);
-#else
-          const float u = (float(i) + ju) / float(a.W - 1);  // main.cpp:278
-          const float v = (float(j) + jv) / float(a.H - 1);  // main.cpp:279
-          get_ray<true, float>(a.cam, u, v, rng, o, d);
-#endif
           T = mk(1.f, 1.f, 1.f);
           depth = 0;
           px = p | (cur << 6);
@@ -751,14 +823,6 @@ __global__ __launch_bounds__(64 * PersistShape<ACC>::waves, PersistShape<ACC>::p
           exhausted = true;
           break;
         }
-#if RTMI_FAIR == 1
-        // The SIMD issues the oldest ready wave first, so in a resident grid
-        // some waves starve (10x spread of work per wave) and end up holding
-        // the last items alone.  A wave behind the average item count raises
-        // its issue priority until it has caught up.
-        if (n_taken * int(gridDim.x) * WPB < int(itn)) __builtin_amdgcn_s_setprio(2);
-        else __builtin_amdgcn_s_setprio(0);
-#endif
         ++n_taken;
         prev_valid = cur_valid;  // all its jobs are handed out
         cur ^= 1;
@@ -785,93 +849,23 @@ __global__ __launch_bounds__(64 * PersistShape<ACC>::waves, PersistShape<ACC>::p
         if (live != live_cur) atomicAdd(&slot_segs[wave][cur ^ 1], unsigned(__popcll(live & ~live_cur)));
       }
     }
-#if RTMI_FAIR == 3
     // The SIMD issues the oldest ready wave first: in a resident grid the
     // youngest wave of a SIMD gets ~1/10 of the oldest one's issue slots and
     // is left holding items alone at the end.  Rotating the issue priority
     // every segment step gives every wave the same share.
-#if RTMI_FAIR_TIME
-    switch ((unsigned(__builtin_amdgcn_s_memrealtime() >> RTMI_FAIR_TIME) + prio_phase) & 3) {
-#else
     switch ((prio_phase++) & 3) {
-#endif
       case 0: __builtin_amdgcn_s_setprio(0); break;
       case 1: __builtin_amdgcn_s_setprio(1); break;
       case 2: __builtin_amdgcn_s_setprio(2); break;
       default: __builtin_amdgcn_s_setprio(3); break;
     }
-#endif
 
     // 2. one segment of every live path
     bool done = false;
     V3<float> col = mk(0.f, 0.f, 0.f);
     if (active) {
-      float t;
       ++nseg;
-#if RTMI_TRACE
-      const unsigned long long cyc0 = __builtin_amdgcn_s_memtime();
-#endif
-      int k;
-      if constexpr (ACC == 1) {
-        k = hit_world_bvh<kBigGroup>(a.acc, o, d, t
-#if RTMI_STATS
-                                      , bvh_stats
-#endif
-        );
-      } else if constexpr (ACC == 2) {
-        k = hit_world_grid<kBigGroup>(a.acc, o, d, t
-#if RTMI_STATS
-                                       , bvh_stats
-#endif
-#if RTMI_TRACE_PHASES
-                                       , phase_clock
-#endif
-        );
-      } else {
-        k = hit_world_packed<kPairGroup>(pairs, a.npairs, o, d, t
-#if RTMI_STATS
-                                         , stats
-#endif
-        );
-      }
-#if RTMI_TRACE
-      cyc_hit += __builtin_amdgcn_s_memtime() - cyc0;
-#endif
-#if RTMI_CHECK
-      if (k >= a.n) atomicAdd(&segments[7], 1ull << 32);
-#endif
-      // 1/|d| once for the lanes that need it: the sky of a miss (main.cpp:80)
-      // and unit(din) of metal and dielectric — the same expression
-      const bool miss = k < 0 || (RTMI_CHECK && k >= a.n);
-      // the hit sphere's three records in one memory round trip (a miss reads
-      // sphere 0's, unused)
-      const int kk = miss ? 0 : k;
-      const float4 sh1k = sc.sh1[kk], sh0k = sc.sh0[kk], geomk = sc.geom[kk];
-      const int kind = miss ? -1 : int(sh1k.x);
-      float inv_len = 0.0f;
-      if (kind != RT_MAT_LAMBERTIAN) inv_len = 1.0f / dsqrt(dot<true>(d, d));
-      if (miss) {
-        const V3<float> sk = sky_fast(d, inv_len);
-        col = mk(T.x * sk.x, T.y * sk.y, T.z * sk.z);
-        done = true;
-      } else {
-        V3<float> p, nrm, at, nd;
-        bool front;
-        hit_record_fast(geomk, sh0k.x, o, d, t, p, nrm, front);
-        if (!scatter_fast(sh0k, sh1k, d, nrm, front, rng, at, nd, inv_len)) {
-          done = true;
-        } else {
-          T = mk(T.x * at.x, T.y * at.y, T.z * at.z);
-          float m = __builtin_fabsf(p.x);  // ray offset, DESIGN.md §3.3
-          if (__builtin_fabsf(p.y) > m) m = __builtin_fabsf(p.y);
-          if (__builtin_fabsf(p.z) > m) m = __builtin_fabsf(p.z);
-          float delta = 0x1p-14f * (1.0f + m);
-          if (dot<true>(nd, nrm) < 0.f) delta = -delta;
-          o = mk(__builtin_fmaf(delta, nrm.x, p.x), __builtin_fmaf(delta, nrm.y, p.y), __builtin_fmaf(delta, nrm.z, p.z));
-          d = nd;
-          if (++depth >= a.max_depth) done = true;
-        }
-      }
+      done = path_segment<ACC>(sc, pairs, a, o, d, T, depth, rng, col, cnt, segments);
     }
     // 3. finished paths add their colour to their item's slot
 #if RTMI_CHECK
@@ -905,19 +899,7 @@ __global__ __launch_bounds__(64 * PersistShape<ACC>::waves, PersistShape<ACC>::p
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   if (lane == 0) atomicAdd(segments, wave_segs[wave]);
-#if RTMI_STATS
-  // brute force: [1] groups, [2] groups with a candidate, [4] sphere
-  // resolves (wave); BVH: [1] node iterations, [2] leaf-sphere iterations,
-  // [4] root resolutions (wave).  [3] resolves (lane), [5] node visits,
-  // [6] leaf sphere tests (lane).
-  if (lane == 0) { atomicAdd(&segments[1], (unsigned long long)stats[0]); atomicAdd(&segments[2], (unsigned long long)stats[1]); atomicAdd(&segments[4], (unsigned long long)stats[3]); }
-  atomicAdd(&segments[3], (unsigned long long)stats[2]);
-  atomicAdd(&segments[5], (unsigned long long)bvh_stats[0]);
-  atomicAdd(&segments[6], (unsigned long long)bvh_stats[1]);
-  atomicAdd(&segments[1], (unsigned long long)bvh_stats[2]);
-  atomicAdd(&segments[2], (unsigned long long)bvh_stats[3]);
-  atomicAdd(&segments[4], (unsigned long long)bvh_stats[4]);
-#endif
+  flush_counters(cnt, lane, segments);
   RTMI_TRACE_END(n_taken)
   (void)n_taken;
 }
@@ -1112,6 +1094,17 @@ struct rt_ctx {
   // samples (RTMI_WANT_ITEMS / RTMI_ITEM_MIN override, for A/B)
   int64_t want_items = std::getenv("RTMI_WANT_ITEMS") ? std::atoll(std::getenv("RTMI_WANT_ITEMS")) : 60000;
   int32_t item_min = std::getenv("RTMI_ITEM_MIN") ? std::atoi(std::getenv("RTMI_ITEM_MIN")) : 24;
+  // ramp-down hand-off: RTMI_HANDOFF=0 off, 1 on (the
+  // grid kernel's chunked launches); RTMI_HANDOFF_LANES: live paths at or
+  // below which an item's paths are handed off; RTMI_HANDOFF_CAP: buffer
+  // capacity in paths (same image in every setting)
+  int32_t handoff_on = std::getenv("RTMI_HANDOFF") ? std::atoi(std::getenv("RTMI_HANDOFF")) : 1;
+  int32_t handoff_lanes = std::getenv("RTMI_HANDOFF_LANES") ? std::atoi(std::getenv("RTMI_HANDOFF_LANES")) : 24;
+  int64_t handoff_cap_max = std::getenv("RTMI_HANDOFF_CAP") ? std::atoll(std::getenv("RTMI_HANDOFF_CAP")) : (int64_t(1) << 22);
+  float *handoff = nullptr;        // kHandoffFields x handoff_cap floats
+  unsigned *handoff_count = nullptr;
+  size_t handoff_cap = 0;          // paths
+  size_t last_handoff_cap = 0;     // capacity the last render used (0: no hand-off)
 };
 
 namespace rtmi {
@@ -1213,7 +1206,8 @@ RTMI_EXPORT int rt_ctx_destroy(rt_ctx *ctx) {
                   (void *)ctx->sh164, (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments, (void *)ctx->pairs, (void *)ctx->counter, (void *)ctx->pass_accum,
                   (void *)ctx->big_pairs, (void *)ctx->big_idx, (void *)ctx->nodes, (void *)ctx->bvh_sph, (void *)ctx->bvh_idx,
                   (void *)ctx->cost_prev, (void *)ctx->cost_cur, (void *)ctx->cost_sorted, (void *)ctx->order,
-                  (void *)ctx->iota, ctx->sort_tmp, (void *)ctx->grid_sph, (void *)ctx->grid_cells, (void *)ctx->grid_refs})
+                  (void *)ctx->iota, ctx->sort_tmp, (void *)ctx->grid_sph, (void *)ctx->grid_cells, (void *)ctx->grid_refs,
+                  (void *)ctx->handoff, (void *)ctx->handoff_count})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(ctx->stream);
   if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
@@ -1673,6 +1667,18 @@ void launch_tw(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const
                        ctx->sh0, ctx->sh1, ctx->pairs, a, accum, out, ctx->segments);
 }
 
+void launch_handoff(int acc, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a, unsigned long long *accum) {
+  const size_t lds = accel_lds_bytes(a.acc, acc);
+  const size_t per_block = size_t(kHandoffPerWave) * kHandoffWaves;
+  const dim3 grid(unsigned((size_t(a.handoff_cap) + per_block - 1) / per_block)), block(64 * kHandoffWaves);
+  if (acc == 1)
+    hipLaunchKernelGGL((handoff_kernel<1>), grid, block, lds, st, ctx->geom, ctx->sh0, ctx->sh1, ctx->pairs, a, accum, ctx->segments);
+  else if (acc == 2)
+    hipLaunchKernelGGL((handoff_kernel<2>), grid, block, lds, st, ctx->geom, ctx->sh0, ctx->sh1, ctx->pairs, a, accum, ctx->segments);
+  else
+    hipLaunchKernelGGL((handoff_kernel<0>), grid, block, lds, st, ctx->geom, ctx->sh0, ctx->sh1, ctx->pairs, a, accum, ctx->segments);
+}
+
 template <int TW>
 void launch_shape(bool persistent, int acc, bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx,
                   const RenderArgs &a, unsigned long long *accum, float *out) {
@@ -1795,6 +1801,36 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   a.block_flush = !persistent && nch2 == 0 && nch1 % grid_wpb == 0 && ctx->block_flush;
   a.block_pool = a.block_flush && ctx->block_pool;
   a.block_owns_tile = a.block_flush && !pass_accum && nch1 == grid_wpb && ctx->block_owns;
+  const bool chunked = pass_accum || nch1 + nch2 > 1;
+  // ramp-down hand-off: the grid kernel's chunked launches;
+  // the handed-off paths add to the accumulator after the main kernel, so no
+  // block writes its tile's floats itself
+  const bool handoff = ctx->handoff_on == 1 && !persistent && chunked && !a.block_pool && ctx->handoff_lanes > 0 &&
+                       ctx->handoff_cap_max > 0;
+  if (handoff) a.block_owns_tile = 0;
+  a.handoff = nullptr;
+  a.handoff_count = nullptr;
+  a.handoff_cap = 0;
+  a.handoff_lanes = 0;
+  if (handoff) {
+    // capacity: at most handoff_lanes paths per item (fewer when the buffer
+    // is capped: a full buffer only means some items finish their own paths)
+    const size_t want = size_t(std::min<int64_t>(items * int64_t(std::min(ctx->handoff_lanes, 64)),
+                                                 std::min<int64_t>(ctx->handoff_cap_max, int64_t(1) << 30)));
+    if (ctx->handoff_cap < want) {
+      int rc;
+      if ((rc = dev_alloc(&ctx->handoff, want * kHandoffFields)) || (!ctx->handoff_count && (rc = dev_alloc(&ctx->handoff_count, 1)))) {
+        ctx->handoff_cap = 0;
+        return rc;
+      }
+      ctx->handoff_cap = want;
+    }
+    a.handoff = ctx->handoff;
+    a.handoff_count = ctx->handoff_count;
+    a.handoff_cap = uint32_t(ctx->handoff_cap);
+    a.handoff_lanes = std::min(ctx->handoff_lanes, 64);
+  }
+  if (!ctx->probing) ctx->last_handoff_cap = handoff ? size_t(a.handoff_cap) : 0;
   if (!ctx->probing) {
     const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush + a.block_owns_tile, a.block_pool, persistent ? 1 : 0,
                               acc_kind};
@@ -1802,7 +1838,6 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   }
   a.s_base = s_base;
   a.out_elems = uint64_t(nvalid) * uint64_t(W) * 3;
-  const bool chunked = pass_accum || nch1 + nch2 > 1;
   const size_t n_valid_out = size_t(nvalid) * W * 3;
   if (chunked && !pass_accum && !a.block_owns_tile) {
     if (ctx->accum_cap < n_valid_out) {
@@ -1881,6 +1916,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   // accumulator)
   if (chunked && !pass_accum && !a.block_owns_tile)
     HIP_TRY(hipMemsetAsync(ctx->accum, 0, n_valid_out * sizeof(unsigned long long), st));
+  if (handoff) HIP_TRY(hipMemsetAsync(ctx->handoff_count, 0, sizeof(unsigned), st));
   dim3 grid;
   if (persistent) {
     // a resident grid of waves pulling items from a global counter
@@ -1902,6 +1938,10 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     default: launch_shape<64>(persistent, acc_kind, chunked, grid, st, ctx, a, accum, strip); break;
   }
   HIP_TRY(hipGetLastError());
+  if (handoff) {  // the handed-off paths, into the same accumulator
+    launch_handoff(acc_kind, st, ctx, a, accum);
+    HIP_TRY(hipGetLastError());
+  }
   if (chunked && !pass_accum && !a.block_owns_tile) {
     hipLaunchKernelGGL(finalize_kernel, dim3(unsigned((n_valid_out + 255) / 256)), dim3(256), 0, st, ctx->accum,
                        strip, n_valid_out);
@@ -2192,6 +2232,24 @@ RTMI_EXPORT int rt_ctx_last_segments(rt_ctx *ctx, uint64_t *segments) {
   HIP_TRY(hipMemcpyAsync(&v, ctx->segments, sizeof v, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   *segments = v;
+  return RT_OK;
+}
+
+// Hand-off of the last render (diagnostics): out[0] = paths the main kernel's
+// waves offered (reserved slots; those past the capacity were finished by
+// their own waves), out[1] = the buffer's capacity; both 0 when the last
+// render did not hand off.
+RTMI_EXPORT int rt_ctx_last_handoff(rt_ctx *ctx, uint64_t *out2) {
+  if (!ctx || !out2) return set_error(RT_EINVAL, "null argument");
+  out2[0] = out2[1] = 0;
+  if (!ctx->last_handoff_cap) return RT_OK;
+  DeviceGuard guard(ctx->device);
+  hipStream_t st = ctx->last_stream ? ctx->last_stream : ctx->stream;
+  uint32_t v = 0;
+  HIP_TRY(hipMemcpyAsync(&v, ctx->handoff_count, sizeof v, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  out2[0] = v;
+  out2[1] = ctx->last_handoff_cap;
   return RT_OK;
 }
 

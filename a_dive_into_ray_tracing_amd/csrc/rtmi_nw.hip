@@ -119,9 +119,6 @@ __device__ __forceinline__ int64_t fixed(float c) {
 // regeneration: the kernel's scalar registers otherwise overflow and the
 // compiler parks them in VGPR lanes (v_readlane at every regeneration), as in
 // the RTIOW kernel.  Staged before stage_scene's barrier.
-#ifndef RTMI_NW_CAM_LDS
-#define RTMI_NW_CAM_LDS 1
-#endif
 __device__ __forceinline__ void stage_camera(float *cl, const Args &a) {
   const unsigned t = threadIdx.x;
   if (t < 23) {
@@ -205,7 +202,6 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
     rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(s));
     float ju, jv;
     rng.pair(ju, jv);
-#if RTMI_NW_CAM_LDS
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // read here, not hoisted out of the loop
     const float u = (float(i) + ju) / cl[21];
     const float v = (float(j) + jv) / cl[22];
@@ -219,13 +215,6 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
     cm.lens = cl[18];
     get_ray<true, float>(cm, u, v, rng, o, d);
     time = __builtin_fmaf(rng.uni(), cl[20], cl[19]);  // camera.h:75-79
-#else
-    (void)cl;
-    const float u = (float(i) + ju) / float(a.W);
-    const float v = (float(j) + jv) / float(a.H);
-    get_ray<true, float>(a.cam, u, v, rng, o, d);
-    time = __builtin_fmaf(rng.uni(), a.time1 - a.time0, a.time0);  // camera.h:75-79
-#endif
     T = mk(1.f, 1.f, 1.f);
     depth = 0;
   };
@@ -406,9 +395,6 @@ __global__ void trace_kernel(View sc, Args a, int i, int j, int s, float *rec, i
     if (k < 0) break;
     const Rec rc = k < sc.nobj ? make_rec(sc, sc.obj[k], o, d, time, t, face) : make_rec_medium(sc, sc.med[k - sc.nobj], o, d, time);
     r[8] = rc.n.x; r[9] = rc.n.y; r[10] = rc.n.z;
-#ifdef RTMI_NW_DBG
-    if (k < sc.nobj) { r[8] = float(sc.obj[k].ka & 255); r[9] = float(sc.obj[k].inst); r[10] = float(k); r[11] = float(sc.obj[k].mat); }
-#endif
     const Mat m = sc.mat[rc.mat];
     V at, nd;
     if (m.kind == kDiffuseLight || !scatter_nw(sc, rc, d, rng, at, nd)) break;

@@ -301,8 +301,8 @@ __device__ __forceinline__ bool path_segment(const SceneView<float> &sc, const S
                                   , cnt.bvh_stats
 #endif
     );
-  } else if constexpr (ACC == 2) {
-    k = hit_world_grid<kBigGroup>(a.acc, o, d, t
+  } else if constexpr (ACC >= 2) {
+    k = hit_world_grid<kBigGroup, ACC == 3>(a.acc, o, d, t
 #if RTMI_STATS
                                    , cnt.bvh_stats
 #endif
@@ -358,7 +358,8 @@ __device__ __forceinline__ bool path_segment(const SceneView<float> &sc, const S
   return ++depth >= a.max_depth;  // depth exhausted: black, main.cpp:58-60
 }
 
-// ACC: 0 brute force, 1 BVH, 2 uniform grid (RT_ACCEL_*); the accelerated
+// ACC: 0 brute force, 1 BVH, 2 uniform grid (RT_ACCEL_*), 3 the grid walked as one
+// y layer (hit_world_grid<.., true>); the accelerated
 // kernels stage their structure in LDS and share the block shape.
 template <int TW, bool CHUNKED, int ACC>
 __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0>::per_eu) void render_kernel(
@@ -379,7 +380,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   stage_camera(cam_lds, a);
   if constexpr (ACC == 0) __syncthreads();  // (accelerated kernels: stage_* ends with one)
   if constexpr (ACC == 1) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
-  else if constexpr (ACC == 2) stage_grid(a.acc);
+  else if constexpr (ACC >= 2) stage_grid(a.acc);
   else if (pool) __syncthreads();
   if (item >= a.n_items) return;  // wave-uniform; no block barrier follows
 
@@ -603,7 +604,7 @@ __global__ __launch_bounds__(64 * kHandoffWaves) void handoff_kernel(
     const SpherePair *__restrict__ pairs, RenderArgs a, unsigned long long *__restrict__ accum,
     unsigned long long *__restrict__ segments) {
   if constexpr (ACC == 1) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
-  else if constexpr (ACC == 2) stage_grid(a.acc);
+  else if constexpr (ACC >= 2) stage_grid(a.acc);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const unsigned total = min(*a.handoff_count, a.handoff_cap);
@@ -730,7 +731,7 @@ __global__ __launch_bounds__(64 * PersistShape<ACC>::waves, PersistShape<ACC>::p
   stage_camera(cam_lds, a);
   if constexpr (ACC == 0) __syncthreads();  // (accelerated kernels: stage_* ends with one)
   if constexpr (ACC == 1) stage_bvh(a.acc);
-  else if constexpr (ACC == 2) stage_grid(a.acc);
+  else if constexpr (ACC >= 2) stage_grid(a.acc);
   if (lane < 2) slot_segs[wave][lane] = 0;
   for (int s = 0; s < 2; ++s)
     for (int c = 0; c < 3; ++c) acc[wave][s][c][lane] = 0;
@@ -920,14 +921,14 @@ __global__ __launch_bounds__(256) void debug_hit_kernel(const SpherePair *__rest
 #if RTMI_STATS
   unsigned st[4] = {0, 0, 0, 0}, bst[5] = {0, 0, 0, 0, 0};
   out_idx[2 * i] = hit_world_packed<kPairGroup>(pairs, npairs, o, d, t0, st);
-  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1, bst) : hit_world_grid<kBigGroup>(acc, o, d, t1, bst);
+  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1, bst) : hit_world_grid<kBigGroup, ACC == 3>(acc, o, d, t1, bst);
 #else
   out_idx[2 * i] = hit_world_packed<kPairGroup>(pairs, npairs, o, d, t0);
 #if RTMI_TRACE_PHASES
   PhaseClock pc{{0, 0, 0}};
-  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup>(acc, o, d, t1, pc);
+  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup, ACC == 3>(acc, o, d, t1, pc);
 #else
-  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup>(acc, o, d, t1);
+  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup, ACC == 3>(acc, o, d, t1);
 #endif
 #endif
   out_t[2 * i] = t0;
@@ -1622,11 +1623,12 @@ namespace {
 
 size_t accel_lds_bytes(const Accel &acc, int kind) {
   if (kind == 1) return bvh_lds_bytes(acc.nnodes, acc.nsph);
-  if (kind == 2) return grid_lds_bytes(acc.nsph, acc.grid.ncells, acc.grid.nrefs);
+  if (kind >= 2) return grid_lds_bytes(acc.nsph, acc.grid.ncells, acc.grid.nrefs);
   return 0;
 }
 
-// The Accel view of the context's structure of `kind` (1 BVH, 2 grid).
+// The Accel view of the context's structure of `kind` (1 BVH, 2 grid, 3 the
+// grid walked as one y layer).
 Accel accel_of(const rt_ctx *ctx, int kind) {
   Accel a{ctx->big_pairs, ctx->big_idx, ctx->nbig_pairs, 0, nullptr, nullptr, nullptr, 0, GridDesc{}};
   if (kind == 1) {
@@ -1635,7 +1637,7 @@ Accel accel_of(const rt_ctx *ctx, int kind) {
     a.sph = ctx->bvh_sph;
     a.sph_idx = ctx->bvh_idx;
     a.nsph = ctx->nbvh_sph;
-  } else if (kind == 2) {
+  } else if (kind >= 2) {
     a.sph = ctx->grid_sph;
     a.nsph = ctx->ngrid_sph;
     a.grid = ctx->grid;
@@ -1675,6 +1677,8 @@ void launch_handoff(int acc, hipStream_t st, const rt_ctx *ctx, const RenderArgs
     hipLaunchKernelGGL((handoff_kernel<1>), grid, block, lds, st, ctx->geom, ctx->sh0, ctx->sh1, ctx->pairs, a, accum, ctx->segments);
   else if (acc == 2)
     hipLaunchKernelGGL((handoff_kernel<2>), grid, block, lds, st, ctx->geom, ctx->sh0, ctx->sh1, ctx->pairs, a, accum, ctx->segments);
+  else if (acc == 3)
+    hipLaunchKernelGGL((handoff_kernel<3>), grid, block, lds, st, ctx->geom, ctx->sh0, ctx->sh1, ctx->pairs, a, accum, ctx->segments);
   else
     hipLaunchKernelGGL((handoff_kernel<0>), grid, block, lds, st, ctx->geom, ctx->sh0, ctx->sh1, ctx->pairs, a, accum, ctx->segments);
 }
@@ -1684,11 +1688,12 @@ void launch_shape(bool persistent, int acc, bool chunked, dim3 grid, hipStream_t
                   const RenderArgs &a, unsigned long long *accum, float *out) {
   if (persistent) {
     if (acc == 1) launch_persistent<TW, 1>(chunked, grid, st, ctx, a, accum, out);
-    else if (acc == 2) launch_persistent<TW, 2>(chunked, grid, st, ctx, a, accum, out);
+    else if (acc >= 2) launch_persistent<TW, 2>(chunked, grid, st, ctx, a, accum, out);  // (the general walk)
     else launch_persistent<TW, 0>(chunked, grid, st, ctx, a, accum, out);
   } else {
     if (acc == 1) launch_tw<TW, 1>(chunked, grid, st, ctx, a, accum, out);
     else if (acc == 2) launch_tw<TW, 2>(chunked, grid, st, ctx, a, accum, out);
+    else if (acc == 3) launch_tw<TW, 3>(chunked, grid, st, ctx, a, accum, out);
     else launch_tw<TW, 0>(chunked, grid, st, ctx, a, accum, out);
   }
 }
@@ -1739,7 +1744,12 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   const int64_t tile_samples = tiles * int64_t(spp);
   // accelerated closest hit (1 BVH, 2 grid; 0 brute force) when the scene
   // has one; both stage their structure in LDS and use the same block shape
-  const int acc_kind = ctx->accel == RT_ACCEL_BVH && ctx->nnodes > 0 ? 1 : (ctx->accel == RT_ACCEL_GRID && ctx->grid_ok ? 2 : 0);
+  // (3: the grid has one cell layer in y and the grid kernel walks it with
+  // the y stepping dropped, hit_world_grid<.., true>: the same cells, 3% faster
+  // on config 2; the persistent kernel keeps the general walk)
+  const int acc_kind = ctx->accel == RT_ACCEL_BVH && ctx->nnodes > 0
+                           ? 1
+                           : (ctx->accel == RT_ACCEL_GRID && ctx->grid_ok ? (ctx->grid.n[1] == 1 ? 3 : 2) : 0);
   const bool bvh = acc_kind != 0;
   const bool persistent = ctx->kernel == RT_KERNEL_PERSISTENT ||
                           (ctx->kernel == RT_KERNEL_AUTO && !bvh && tile_samples < 6000000);
@@ -1749,7 +1759,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     // 1/8 strip: chunk 8 -> 4.41 ms, 16 -> 4.27, 32 -> 4.43, 64 -> 6.69; frame
     // 31.0-32.9 for 8..64; profiles/r02/ab_persistent/pers_chunk)
     const int64_t waves = int64_t(acc_kind == 1 ? ctx->resident_blocks_bvh : ctx->resident_blocks_grid) *
-                          (acc_kind == 1 ? PersistShape<1>::waves : PersistShape<2>::waves);
+                          (acc_kind == 1 ? PersistShape<1>::waves : PersistShape<2>::waves);  // (2 and 3)
     chunk1 = int32_t(std::min<int64_t>(32, std::max<int64_t>(8, tile_samples / (8 * waves))));
   } else if (chunk1 <= 0 && persistent) {
     // ~28 items per resident wave (1/8 strip: chunk 8 -> 17.5 ms, 16 -> 17.9, 32 -> 19.7)
@@ -1833,7 +1843,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   if (!ctx->probing) ctx->last_handoff_cap = handoff ? size_t(a.handoff_cap) : 0;
   if (!ctx->probing) {
     const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush + a.block_owns_tile, a.block_pool, persistent ? 1 : 0,
-                              acc_kind};
+                              acc_kind == 3 ? 2 : acc_kind};
     std::copy(sched, sched + 8, ctx->last_sched);
   }
   a.s_base = s_base;
@@ -1921,11 +1931,11 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   if (persistent) {
     // a resident grid of waves pulling items from a global counter
     HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
-    const int64_t pw = acc_kind == 1 ? PersistShape<1>::waves : acc_kind == 2 ? PersistShape<2>::waves
+    const int64_t pw = acc_kind == 1 ? PersistShape<1>::waves : acc_kind >= 2 ? PersistShape<2>::waves
                                                                                 : PersistShape<0>::waves;
     const int64_t waves =
         std::min<int64_t>(items, int64_t(acc_kind == 1 ? ctx->resident_blocks_bvh
-                                         : acc_kind == 2 ? ctx->resident_blocks_grid : ctx->resident_blocks) * pw);
+                                         : acc_kind >= 2 ? ctx->resident_blocks_grid : ctx->resident_blocks) * pw);
     grid = dim3(unsigned((waves + pw - 1) / pw));
   } else {
     const int64_t wpb = bvh ? GridShape<true>::waves : GridShape<false>::waves;
@@ -2293,18 +2303,22 @@ RTMI_EXPORT int rt_ctx_debug_hits(rt_ctx *ctx, const float *rays, int32_t n, int
       (rc = dev_alloc(&d_t, size_t(n) * 2)))
     return rc;
   HIP_TRY(hipMemcpy(d_rays, rays, size_t(n) * 6 * sizeof(float), hipMemcpyHostToDevice));
-  const int kind = ctx->accel == RT_ACCEL_GRID ? 2 : 1;
-  if ((kind == 1 && !ctx->nnodes) || (kind == 2 && !ctx->grid_ok)) {
+  // the walk the renders use (3: the one-layer grid walk)
+  const int kind = ctx->accel == RT_ACCEL_GRID ? (ctx->grid_ok && ctx->grid.n[1] == 1 ? 3 : 2) : 1;
+  if ((kind == 1 && !ctx->nnodes) || (kind >= 2 && !ctx->grid_ok)) {
     (void)hipFree(d_rays); (void)hipFree(d_idx); (void)hipFree(d_t);
-    return set_error(RT_EUNSUPPORTED, "rt_ctx_debug_hits: no %s for this scene", kind == 2 ? "grid" : "BVH");
+    return set_error(RT_EUNSUPPORTED, "rt_ctx_debug_hits: no %s for this scene", kind >= 2 ? "grid" : "BVH");
   }
   const Accel acc = accel_of(ctx, kind);
   const size_t lds = accel_lds_bytes(acc, kind);
   if (kind == 1)
     hipLaunchKernelGGL(debug_hit_kernel<1>, dim3(unsigned((n + 255) / 256)), dim3(256), lds, ctx->stream, ctx->pairs,
                        ctx->npairs, acc, d_rays, n, d_idx, d_t);
-  else
+  else if (kind == 2)
     hipLaunchKernelGGL(debug_hit_kernel<2>, dim3(unsigned((n + 255) / 256)), dim3(256), lds, ctx->stream, ctx->pairs,
+                       ctx->npairs, acc, d_rays, n, d_idx, d_t);
+  else
+    hipLaunchKernelGGL(debug_hit_kernel<3>, dim3(unsigned((n + 255) / 256)), dim3(256), lds, ctx->stream, ctx->pairs,
                        ctx->npairs, acc, d_rays, n, d_idx, d_t);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));

@@ -613,8 +613,10 @@ __device__ __forceinline__ void hit_big(const Accel &acc_s, V3<float> d, float K
 // error of the cell boundaries (each computed directly from the cell index,
 // never accumulated), so the cell the DDA holds for any accepted hit point
 // lists that sphere; a sphere tested in several cells gives the same root
-// each time.
-template <int GP>
+// each time.  FLAT_Y: the grid has one cell layer in y (the final scene's
+// 20 x 1 x 20) — the same walk with the y axis' stepping state dropped: a y
+// face only ends the walk (5 VGPRs fewer in the loop).
+template <int GP, bool FLAT_Y = false>
 __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> o, V3<float> d, float &t_hit
 #if RTMI_STATS
                                                   , unsigned *gstats
@@ -659,7 +661,7 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
       return c < 0 ? 0 : (c >= G.n[ax] ? G.n[ax] - 1 : c);
     };
     const int cx = cell_of(__builtin_fmaf(tnear, d.x, o.x), 0);
-    const int cy = cell_of(__builtin_fmaf(tnear, d.y, o.y), 1);
+    const int cy = FLAT_Y ? 0 : cell_of(__builtin_fmaf(tnear, d.y, o.y), 1);
     const int cz = cell_of(__builtin_fmaf(tnear, d.z, o.z), 2);
     // Per axis: after k steps on it the current cell's far face lies at
     // t = fma(k, dt, t0) (t0 the entry cell's far face, dt = h/|d_axis|), and
@@ -675,7 +677,12 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
       kmax = float(pos ? G.n[ax] - 1 - c : c);
     };
     axis(d.x, ix, ox, cx, 0, t0x, dtx, kmx);
-    axis(d.y, iy, oy, cy, 1, t0y, dty, kmy);
+    if constexpr (FLAT_Y) {  // the one layer's far y face (axis() at c = 0, no steps)
+      t0y = __builtin_fmaf(__builtin_fmaf(d.y >= 0.0f ? 1.0f : 0.0f, G.h[1], G.g0[1]), iy, oy);
+      dty = kmy = 0.0f;
+    } else {
+      axis(d.y, iy, oy, cy, 1, t0y, dty, kmy);
+    }
     axis(d.z, iz, oz, cz, 2, t0z, dtz, kmz);
     float kx = 0.0f, ky = 0.0f, kz = 0.0f, tnx = t0x, tny = t0y, tnz = t0z;
     // the LDS address of the current cell's start, stepped by 4 x the cell step
@@ -714,7 +721,7 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
         tnx = __builtin_fmaf(kx, dtx, t0x);
         cell += dcx;
       } else if (tny <= tnz) {
-        if (ky >= kmy) break;
+        if (FLAT_Y || ky >= kmy) break;  // leaves the grid
         ky += 1.0f;
         tny = __builtin_fmaf(ky, dty, t0y);
         cell += dcy;

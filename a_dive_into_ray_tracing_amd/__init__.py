@@ -239,13 +239,6 @@ class Renderer:
         keys = ("tile_w", "chunk", "items_per_tile", "tail_items_per_tile", "block_flush", "block_pool", "persistent", "bvh")
         return dict(zip(keys, list(v)))
 
-    def last_handoff(self):
-        """Diagnostic: (paths handed off to the tail kernel, buffer capacity) of the
-        last render (rt_ctx_last_handoff); (0, 0) when it did not hand off."""
-        v = (C.c_uint64 * 2)()
-        check(self.L.rt_ctx_last_handoff(self._h, v), "rt_ctx_last_handoff")
-        return int(v[0]), int(v[1])
-
     def synchronize(self):
         check(self.L.rt_ctx_synchronize(self._h), "rt_ctx_synchronize")
 

@@ -153,7 +153,6 @@ SIGNATURES = {
         [C.c_void_p, C.POINTER(RtNwCamera)] + [C.c_int32] * 4 + [C.c_uint64] + [C.c_int32] * 3 + [C.c_void_p, C.c_void_p],
     ),
     "rt_ctx_last_schedule": (C.c_int, [C.c_void_p, _ip]),
-    "rt_ctx_last_handoff": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     "rt_ctx_grid_info": (C.c_int, [C.c_void_p, _ip, _ip, _ip]),
     "rt_nw_ctx_last_segments": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     "rt_nw_ctx_last_kernel": (C.c_int, [C.c_void_p, _ip]),

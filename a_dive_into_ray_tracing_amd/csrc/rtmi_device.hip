@@ -82,21 +82,7 @@ struct RenderArgs {
   // and per-tile world.hit counts of this launch (null: not measured)
   const int32_t *tile_order;
   unsigned *tile_cost;
-  // hand-off of an item's last paths (chunked grid-kernel
-  // launches): once all of an item's jobs are taken and at most
-  // handoff_lanes of its paths are live, they are written to the hand-off
-  // buffer (kHandoffFields arrays of handoff_cap, structure of arrays) and the
-  // wave leaves; handoff_kernel finishes them.  null: off.
-  float *handoff;
-  unsigned *handoff_count;  // slots reserved (may exceed the capacity: those paths stayed)
-  uint32_t handoff_cap;
-  int32_t handoff_lanes;
 };
-// a handed-off path: o, d, T (9 floats), the generator (4 words), depth,
-// pixel (row-major index into the launch's W x rows strip; ~0u: an empty
-// slot), and one spare field
-constexpr int kHandoffFields = 16;
-constexpr uint32_t kHandoffEmpty = 0xFFFFFFFFu;
 
 #ifndef RTMI_WAVES_PER_BLOCK
 #define RTMI_WAVES_PER_BLOCK 4
@@ -490,43 +476,6 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
       }
       next += __popcll(m);
     }
-    if constexpr (CHUNKED) {
-      // ramp-down hand-off: all jobs taken (wave-uniform),
-      // few paths live -> write them out and leave
-      if (a.handoff && !pool && next >= nq) {
-        const unsigned long long live = __ballot(active);
-        const int n = __popcll(live);
-        if (n > 0 && n <= a.handoff_lanes) {
-          unsigned base = 0;
-          if (lane == 0) base = atomicAdd(a.handoff_count, unsigned(n));
-          base = __builtin_amdgcn_readfirstlane(base);
-          const bool fits = uint64_t(base) + uint64_t(n) <= uint64_t(a.handoff_cap);  // wave-uniform
-          if (active) {
-            const unsigned slot = base + __builtin_amdgcn_mbcnt_hi(unsigned(live >> 32),
-                                                                   __builtin_amdgcn_mbcnt_lo(unsigned(live), 0u));
-            if (slot < a.handoff_cap) {  // a reserved slot below the capacity is always written
-              float *h = a.handoff + slot;
-              const size_t cap = a.handoff_cap;
-              uint32_t pix = kHandoffEmpty;
-              if (fits) {
-                const int ly = div_small(px, vw, inv_vw), lx = px - ly * vw;
-                pix = uint32_t(y0 + ly) * uint32_t(a.W) + uint32_t(x0 + lx);
-                h[0 * cap] = o.x; h[1 * cap] = o.y; h[2 * cap] = o.z;
-                h[3 * cap] = d.x; h[4 * cap] = d.y; h[5 * cap] = d.z;
-                h[6 * cap] = T.x; h[7 * cap] = T.y; h[8 * cap] = T.z;
-                h[9 * cap] = __uint_as_float(uint32_t(rng.s0));
-                h[10 * cap] = __uint_as_float(uint32_t(rng.s0 >> 32));
-                h[11 * cap] = __uint_as_float(uint32_t(rng.s1));
-                h[12 * cap] = __uint_as_float(uint32_t(rng.s1 >> 32));
-                h[13 * cap] = __int_as_float(depth);
-              }
-              h[14 * cap] = __uint_as_float(pix);
-            }
-          }
-          if (fits) active = false;  // (else: the buffer is full, the wave finishes its paths)
-        }
-      }
-    }
 #if RTMI_TRACE_PHASES
     const unsigned long long cyc_e = __builtin_amdgcn_s_memtime();
     cyc_regen += cyc_e - cyc_b;
@@ -584,89 +533,6 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
       else out[o3 + c] = from_fixed((long long)v);
     }
   }
-}
-
-// ---------------------------------------------------------------------------
-// hand-off kernel: finishes the paths render_kernel handed off
-// ---------------------------------------------------------------------------
-// Each wave takes kHandoffPerWave consecutive slots of the hand-off buffer as
-// its job queue: a lane whose path ends adds its colour to the fixed-point
-// accumulator (global int64 atomics: the sums are order-independent, so the
-// image is the same bit for bit) and loads the next slot (the main kernel's
-// ballot + mbcnt regeneration), so lanes stay busy until the queue's last
-// paths.  Empty slots (kHandoffEmpty) are skipped.
-constexpr int kHandoffPerWave = 256;
-constexpr int kHandoffWaves = 4;  // waves per block
-
-template <int ACC>
-__global__ __launch_bounds__(64 * kHandoffWaves) void handoff_kernel(
-    const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1,
-    const SpherePair *__restrict__ pairs, RenderArgs a, unsigned long long *__restrict__ accum,
-    unsigned long long *__restrict__ segments) {
-  if constexpr (ACC == 1) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
-  else if constexpr (ACC >= 2) stage_grid(a.acc);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const unsigned total = min(*a.handoff_count, a.handoff_cap);
-  const unsigned q_base = (unsigned(blockIdx.x) * kHandoffWaves + unsigned(wave)) * unsigned(kHandoffPerWave);
-  if (q_base >= total) return;  // wave-uniform
-  const int nq = int(min(total - q_base, unsigned(kHandoffPerWave)));
-  const SceneView<float> sc{geom, sh0, sh1, a.n};
-  const size_t cap = a.handoff_cap;
-  SegCounters cnt{};
-  unsigned nseg = 0;
-  V3<float> o, d, T;
-  int depth = 0;
-  uint32_t pix = kHandoffEmpty;
-  Xoro rng;
-  auto load = [&](int q) {
-    const float *h = a.handoff + q_base + unsigned(q);
-    o = mk(h[0 * cap], h[1 * cap], h[2 * cap]);
-    d = mk(h[3 * cap], h[4 * cap], h[5 * cap]);
-    T = mk(h[6 * cap], h[7 * cap], h[8 * cap]);
-    rng.s0 = uint64_t(__float_as_uint(h[9 * cap])) | uint64_t(__float_as_uint(h[10 * cap])) << 32;
-    rng.s1 = uint64_t(__float_as_uint(h[11 * cap])) | uint64_t(__float_as_uint(h[12 * cap])) << 32;
-    depth = __float_as_int(h[13 * cap]);
-    pix = __float_as_uint(h[14 * cap]);
-    // a pixel outside the launch's strip (never written so) is an empty slot
-    if (uint64_t(pix) * 3 >= a.out_elems) pix = kHandoffEmpty;
-  };
-  bool active = lane < nq;
-  if (active) load(lane);
-  int next = 64;
-  for (;;) {
-    if (__ballot(active) == 0) break;
-    bool done = false;
-    V3<float> col = mk(0.f, 0.f, 0.f);
-    if (active) {
-      if (pix == kHandoffEmpty) {
-        done = true;
-      } else {
-        ++nseg;
-        done = path_segment<ACC>(sc, pairs, a, o, d, T, depth, rng, col, cnt, segments);
-      }
-    }
-    const unsigned long long m = __ballot(done);
-    if (m) {
-      if (done) {
-        if (pix != kHandoffEmpty) {
-          unsigned long long *acc3 = accum + size_t(pix) * 3;
-          atomicAdd(&acc3[0], (unsigned long long)to_fixed(col.x));
-          atomicAdd(&acc3[1], (unsigned long long)to_fixed(col.y));
-          atomicAdd(&acc3[2], (unsigned long long)to_fixed(col.z));
-        }
-        const int q = next + __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
-        if (q < nq) load(q);
-        else active = false;
-      }
-      next += __popcll(m);
-    }
-  }
-  // world.hit calls: one atomic per wave
-  unsigned long long ws = nseg;
-  for (int off = 32; off > 0; off >>= 1) ws += __shfl_xor(ws, off);
-  if (lane == 0) atomicAdd(segments, ws);
-  flush_counters(cnt, lane, segments);
 }
 
 // ---------------------------------------------------------------------------
@@ -1095,17 +961,6 @@ struct rt_ctx {
   // samples (RTMI_WANT_ITEMS / RTMI_ITEM_MIN override, for A/B)
   int64_t want_items = std::getenv("RTMI_WANT_ITEMS") ? std::atoll(std::getenv("RTMI_WANT_ITEMS")) : 60000;
   int32_t item_min = std::getenv("RTMI_ITEM_MIN") ? std::atoi(std::getenv("RTMI_ITEM_MIN")) : 24;
-  // ramp-down hand-off: RTMI_HANDOFF=0 off, 1 on (the
-  // grid kernel's chunked launches); RTMI_HANDOFF_LANES: live paths at or
-  // below which an item's paths are handed off; RTMI_HANDOFF_CAP: buffer
-  // capacity in paths (same image in every setting)
-  int32_t handoff_on = std::getenv("RTMI_HANDOFF") ? std::atoi(std::getenv("RTMI_HANDOFF")) : 1;
-  int32_t handoff_lanes = std::getenv("RTMI_HANDOFF_LANES") ? std::atoi(std::getenv("RTMI_HANDOFF_LANES")) : 24;
-  int64_t handoff_cap_max = std::getenv("RTMI_HANDOFF_CAP") ? std::atoll(std::getenv("RTMI_HANDOFF_CAP")) : (int64_t(1) << 22);
-  float *handoff = nullptr;        // kHandoffFields x handoff_cap floats
-  unsigned *handoff_count = nullptr;
-  size_t handoff_cap = 0;          // paths
-  size_t last_handoff_cap = 0;     // capacity the last render used (0: no hand-off)
 };
 
 namespace rtmi {
@@ -1207,8 +1062,7 @@ RTMI_EXPORT int rt_ctx_destroy(rt_ctx *ctx) {
                   (void *)ctx->sh164, (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments, (void *)ctx->pairs, (void *)ctx->counter, (void *)ctx->pass_accum,
                   (void *)ctx->big_pairs, (void *)ctx->big_idx, (void *)ctx->nodes, (void *)ctx->bvh_sph, (void *)ctx->bvh_idx,
                   (void *)ctx->cost_prev, (void *)ctx->cost_cur, (void *)ctx->cost_sorted, (void *)ctx->order,
-                  (void *)ctx->iota, ctx->sort_tmp, (void *)ctx->grid_sph, (void *)ctx->grid_cells, (void *)ctx->grid_refs,
-                  (void *)ctx->handoff, (void *)ctx->handoff_count})
+                  (void *)ctx->iota, ctx->sort_tmp, (void *)ctx->grid_sph, (void *)ctx->grid_cells, (void *)ctx->grid_refs})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(ctx->stream);
   if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
@@ -1669,20 +1523,6 @@ void launch_tw(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const
                        ctx->sh0, ctx->sh1, ctx->pairs, a, accum, out, ctx->segments);
 }
 
-void launch_handoff(int acc, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a, unsigned long long *accum) {
-  const size_t lds = accel_lds_bytes(a.acc, acc);
-  const size_t per_block = size_t(kHandoffPerWave) * kHandoffWaves;
-  const dim3 grid(unsigned((size_t(a.handoff_cap) + per_block - 1) / per_block)), block(64 * kHandoffWaves);
-  if (acc == 1)
-    hipLaunchKernelGGL((handoff_kernel<1>), grid, block, lds, st, ctx->geom, ctx->sh0, ctx->sh1, ctx->pairs, a, accum, ctx->segments);
-  else if (acc == 2)
-    hipLaunchKernelGGL((handoff_kernel<2>), grid, block, lds, st, ctx->geom, ctx->sh0, ctx->sh1, ctx->pairs, a, accum, ctx->segments);
-  else if (acc == 3)
-    hipLaunchKernelGGL((handoff_kernel<3>), grid, block, lds, st, ctx->geom, ctx->sh0, ctx->sh1, ctx->pairs, a, accum, ctx->segments);
-  else
-    hipLaunchKernelGGL((handoff_kernel<0>), grid, block, lds, st, ctx->geom, ctx->sh0, ctx->sh1, ctx->pairs, a, accum, ctx->segments);
-}
-
 template <int TW>
 void launch_shape(bool persistent, int acc, bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx,
                   const RenderArgs &a, unsigned long long *accum, float *out) {
@@ -1812,35 +1652,6 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   a.block_pool = a.block_flush && ctx->block_pool;
   a.block_owns_tile = a.block_flush && !pass_accum && nch1 == grid_wpb && ctx->block_owns;
   const bool chunked = pass_accum || nch1 + nch2 > 1;
-  // ramp-down hand-off: the grid kernel's chunked launches;
-  // the handed-off paths add to the accumulator after the main kernel, so no
-  // block writes its tile's floats itself
-  const bool handoff = ctx->handoff_on == 1 && !persistent && chunked && !a.block_pool && ctx->handoff_lanes > 0 &&
-                       ctx->handoff_cap_max > 0;
-  if (handoff) a.block_owns_tile = 0;
-  a.handoff = nullptr;
-  a.handoff_count = nullptr;
-  a.handoff_cap = 0;
-  a.handoff_lanes = 0;
-  if (handoff) {
-    // capacity: at most handoff_lanes paths per item (fewer when the buffer
-    // is capped: a full buffer only means some items finish their own paths)
-    const size_t want = size_t(std::min<int64_t>(items * int64_t(std::min(ctx->handoff_lanes, 64)),
-                                                 std::min<int64_t>(ctx->handoff_cap_max, int64_t(1) << 30)));
-    if (ctx->handoff_cap < want) {
-      int rc;
-      if ((rc = dev_alloc(&ctx->handoff, want * kHandoffFields)) || (!ctx->handoff_count && (rc = dev_alloc(&ctx->handoff_count, 1)))) {
-        ctx->handoff_cap = 0;
-        return rc;
-      }
-      ctx->handoff_cap = want;
-    }
-    a.handoff = ctx->handoff;
-    a.handoff_count = ctx->handoff_count;
-    a.handoff_cap = uint32_t(ctx->handoff_cap);
-    a.handoff_lanes = std::min(ctx->handoff_lanes, 64);
-  }
-  if (!ctx->probing) ctx->last_handoff_cap = handoff ? size_t(a.handoff_cap) : 0;
   if (!ctx->probing) {
     const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush + a.block_owns_tile, a.block_pool, persistent ? 1 : 0,
                               acc_kind == 3 ? 2 : acc_kind};
@@ -1926,7 +1737,6 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   // accumulator)
   if (chunked && !pass_accum && !a.block_owns_tile)
     HIP_TRY(hipMemsetAsync(ctx->accum, 0, n_valid_out * sizeof(unsigned long long), st));
-  if (handoff) HIP_TRY(hipMemsetAsync(ctx->handoff_count, 0, sizeof(unsigned), st));
   dim3 grid;
   if (persistent) {
     // a resident grid of waves pulling items from a global counter
@@ -1948,10 +1758,6 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     default: launch_shape<64>(persistent, acc_kind, chunked, grid, st, ctx, a, accum, strip); break;
   }
   HIP_TRY(hipGetLastError());
-  if (handoff) {  // the handed-off paths, into the same accumulator
-    launch_handoff(acc_kind, st, ctx, a, accum);
-    HIP_TRY(hipGetLastError());
-  }
   if (chunked && !pass_accum && !a.block_owns_tile) {
     hipLaunchKernelGGL(finalize_kernel, dim3(unsigned((n_valid_out + 255) / 256)), dim3(256), 0, st, ctx->accum,
                        strip, n_valid_out);
@@ -2242,24 +2048,6 @@ RTMI_EXPORT int rt_ctx_last_segments(rt_ctx *ctx, uint64_t *segments) {
   HIP_TRY(hipMemcpyAsync(&v, ctx->segments, sizeof v, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   *segments = v;
-  return RT_OK;
-}
-
-// Hand-off of the last render (diagnostics): out[0] = paths the main kernel's
-// waves offered (reserved slots; those past the capacity were finished by
-// their own waves), out[1] = the buffer's capacity; both 0 when the last
-// render did not hand off.
-RTMI_EXPORT int rt_ctx_last_handoff(rt_ctx *ctx, uint64_t *out2) {
-  if (!ctx || !out2) return set_error(RT_EINVAL, "null argument");
-  out2[0] = out2[1] = 0;
-  if (!ctx->last_handoff_cap) return RT_OK;
-  DeviceGuard guard(ctx->device);
-  hipStream_t st = ctx->last_stream ? ctx->last_stream : ctx->stream;
-  uint32_t v = 0;
-  HIP_TRY(hipMemcpyAsync(&v, ctx->handoff_count, sizeof v, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  out2[0] = v;
-  out2[1] = ctx->last_handoff_cap;
   return RT_OK;
 }
 

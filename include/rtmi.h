@@ -192,11 +192,6 @@ int rt_ctx_last_segments(rt_ctx *ctx, uint64_t *segments);
  *  block flush (2: the block owns its tile and writes the floats), block
  *  pool, persistent kernel, accelerator (0 none, 1 BVH, 2 grid)}. */
 int rt_ctx_last_schedule(rt_ctx *ctx, int32_t *out8);
-/* Diagnostic: the ramp-down hand-off of the context's last render
- * (DESIGN.md §4.7): {paths the main kernel offered to the hand-off kernel,
- * hand-off buffer capacity}; {0, 0} when that render did not hand off.
- * Waits for the render to finish. */
-int rt_ctx_last_handoff(rt_ctx *ctx, uint64_t *out2);
 /* Block until the context's stream is idle. */
 int rt_ctx_synchronize(rt_ctx *ctx);
 

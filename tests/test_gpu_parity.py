@@ -487,7 +487,6 @@ def test_block_flush_same_image(accel, W, H, S, final_world, monkeypatch):
         monkeypatch.setenv("RTMI_BLOCK_FLUSH", flush)
         monkeypatch.setenv("RTMI_BLOCK_POOL", pool)
         monkeypatch.setenv("RTMI_BLOCK_OWNS", owns)
-        monkeypatch.setenv("RTMI_HANDOFF", "0")  # a handing-off launch never owns its tile
         r = rt.Renderer(final_world, 0)
         try:
             r.set_kernel("grid")
@@ -507,69 +506,6 @@ def test_block_flush_same_image(accel, W, H, S, final_world, monkeypatch):
     assert all(sg == segs[0] for sg in segs)
     want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
     assert np.array_equal(imgs[0], want)
-
-
-@pytest.mark.parametrize("accel", ["none", "bvh", "grid"])
-@pytest.mark.parametrize("W,H,S", [(40, 24, 37), (29, 19, 130)])
-def test_handoff_same_image(accel, W, H, S, final_world, monkeypatch):
-    """Ramp-down hand-off: once an item's jobs are all taken
-    and at most RTMI_HANDOFF_LANES of its paths are live, the wave writes them
-    (origin, direction, throughput, RNG state, depth, pixel) to a buffer and
-    leaves; a tail kernel finishes them into the same fixed-point accumulator.
-    Off, on (24 lanes), on with every lane (64: all of an item's last paths)
-    and on with a 100-path buffer (most waves find it full and finish their
-    own paths): the same image and world.hit count bit for bit, equal to the
-    oracle.  The hand-off counter is read back, so the test cannot pass on a
-    path it skipped."""
-    cam = rt.final_camera(W / H)
-    imgs, segs, offered = [], [], []
-    for on, lanes, cap in (("0", "24", "0"), ("1", "24", str(1 << 22)), ("1", "64", str(1 << 22)), ("1", "64", "100")):
-        monkeypatch.setenv("RTMI_HANDOFF", on)
-        monkeypatch.setenv("RTMI_HANDOFF_LANES", lanes)
-        monkeypatch.setenv("RTMI_HANDOFF_CAP", cap)
-        r = rt.Renderer(final_world, 0)
-        try:
-            r.set_kernel("grid")
-            r.set_accel(accel)
-            imgs.append(r.render(cam, W, H, S, 50, SEED))
-            segs.append(r.last_segments())
-            offered.append(r.last_handoff())
-        finally:
-            r.close()
-    assert offered[0] == (0, 0)
-    assert all(o[0] > 0 for o in offered[1:]), offered
-    assert offered[3][1] == 100 and offered[3][0] > 100, offered
-    assert all(np.array_equal(imgs[0], im) for im in imgs[1:])
-    assert all(sg == segs[0] for sg in segs)
-    want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
-    assert np.array_equal(imgs[0], want)
-
-
-def test_handoff_strips_equal_frame_rows(final_world, monkeypatch):
-    """Hand-off on interleaved row strips (the multi-GPU layout): the handed-off
-    paths land on their strip rows — each strip equals the frame's rows."""
-    torch = pytest.importorskip("torch")
-    W, H, S, G = 40, 30, 64, 3
-    cam = rt.final_camera(W / H)
-    monkeypatch.setenv("RTMI_HANDOFF_LANES", "64")
-    r = rt.Renderer(final_world, 0)
-    try:
-        r.set_kernel("grid")
-        r.set_accel("grid")
-        full = r.render(cam, W, H, S, 50, SEED)
-        assert r.last_handoff()[0] > 0
-        nrows = (H + G - 1) // G
-        dev = torch.device("cuda", 0)
-        for g in range(G):
-            strip = torch.full((nrows, W, 3), -1.0, dtype=torch.float32, device=dev)
-            r.render_rows(cam, W, H, S, 50, SEED, g, G, nrows, strip.data_ptr(), torch.cuda.current_stream().cuda_stream)
-            torch.cuda.synchronize()
-            assert r.last_handoff()[0] > 0
-            s = strip.cpu().numpy()
-            for k in range(nrows):
-                assert np.array_equal(s[k], full[g + k * G]), (g, k)
-    finally:
-        r.close()
 
 
 @pytest.mark.parametrize("accel", ["none", "bvh", "grid"])

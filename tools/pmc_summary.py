@@ -1,5 +1,5 @@
 """Summarise rocprofv3 PMC csvs of the render kernels: per-dispatch means,
-grouped by kernel (render, hand-off and finalize kernels).  usage: pmc_summary.py DIR"""
+grouped by kernel (render and finalize kernels).  usage: pmc_summary.py DIR"""
 import collections
 import csv
 import glob
@@ -12,7 +12,7 @@ for f in sorted(glob.glob(f"{root}/pmc*/*_counter_collection.csv")):
     names = {}
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if any(n in k for n in ("render_kernel", "render_persistent", "handoff_kernel", "finalize_kernel")):
+        if any(n in k for n in ("render_kernel", "render_persistent", "finalize_kernel")):
             per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
             names[r["Dispatch_Id"]] = k.split("(")[0]
     for (dsp, c), v in per.items():

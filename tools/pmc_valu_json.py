@@ -1,7 +1,8 @@
 """profiles/pmc_valu.json from tools/profile.sh's PMC passes: per-launch
 VALU counters of the timed render kernel (config 2, grid), which bench.py
 reports beside the algorithmic roofline as roofline.pmc.
-usage: pmc_valu_json.py PROFILE_DIR KERNEL_MS SOURCE_NOTE > profiles/pmc_valu.json"""
+usage: pmc_valu_json.py PROFILE_DIR KERNEL_MS SOURCE_NOTE [KERNEL] > profiles/pmc_valu.json
+(KERNEL default: the one-layer grid instantiation render_kernel<8, true, 3>)"""
 import collections
 import csv
 import glob
@@ -9,7 +10,7 @@ import json
 import sys
 
 root, kernel_ms, note = sys.argv[1], float(sys.argv[2]), sys.argv[3]
-want = "rtmi::render_kernel<8, true, 2>"
+want = sys.argv[4] if len(sys.argv) > 4 else "rtmi::render_kernel<8, true, 3>"
 vals = collections.defaultdict(list)
 for f in sorted(glob.glob(f"{root}/pmc*/*_counter_collection.csv")):
     per = collections.defaultdict(float)

@@ -251,14 +251,13 @@ __device__ __forceinline__ bool hit_rect_inv(V o, V d, V inv, float a0, float a1
   const float ok = KA == 0 ? o.x : KA == 1 ? o.y : o.z;
   const float ik = KA == 0 ? inv.x : KA == 1 ? inv.y : inv.z;
   const float tt = (k - ok) * ik;
-  if (tt < tmin || tt > tmax) return false;
   const float oa = AA == 0 ? o.x : o.y, da = AA == 0 ? d.x : d.y;
   const float ob = BA == 1 ? o.y : o.z, db = BA == 1 ? d.y : d.z;
   const float x = __builtin_fmaf(tt, da, oa);
   const float y = __builtin_fmaf(tt, db, ob);
-  if (x < a0 || x > a1 || y < b0 || y > b1) return false;
-  t = tt;
-  return true;
+  const bool hit = !(tt < tmin) & !(tt > tmax) & !(x < a0) & !(x > a1) & !(y < b0) & !(y > b1);
+  t = hit ? tt : t;
+  return hit;
 }
 __device__ __forceinline__ bool hit_rect_kind_inv(int kind, V o, V d, V inv, const float4 g, float k, float tmin,
                                                   float tmax, float &t) {
@@ -270,12 +269,20 @@ __device__ __forceinline__ int hit_box_inv(V o, V d, V inv, const float4 p0, con
                                            float &t) {
   int face = -1;
   float closest = tmax, tt;
-  if (hit_rect_inv<2, 0, 1>(o, d, inv, p0.x, p1.x, p0.y, p1.y, p1.z, tmin, closest, tt)) { closest = tt; face = 0; }
-  if (hit_rect_inv<2, 0, 1>(o, d, inv, p0.x, p1.x, p0.y, p1.y, p0.z, tmin, closest, tt)) { closest = tt; face = 1; }
-  if (hit_rect_inv<1, 0, 2>(o, d, inv, p0.x, p1.x, p0.z, p1.z, p1.y, tmin, closest, tt)) { closest = tt; face = 2; }
-  if (hit_rect_inv<1, 0, 2>(o, d, inv, p0.x, p1.x, p0.z, p1.z, p0.y, tmin, closest, tt)) { closest = tt; face = 3; }
-  if (hit_rect_inv<0, 1, 2>(o, d, inv, p0.y, p1.y, p0.z, p1.z, p1.x, tmin, closest, tt)) { closest = tt; face = 4; }
-  if (hit_rect_inv<0, 1, 2>(o, d, inv, p0.y, p1.y, p0.z, p1.z, p0.x, tmin, closest, tt)) { closest = tt; face = 5; }
+  tt = closest;
+  // each side's test and the update as compares combined bitwise and selects
+  // (no exec-mask branches): Next-Week final scene 291 -> 283 ms at 256 spp,
+  // profiles/r03/ab_nw_bitwise.txt
+  auto side = [&](bool h, int f) {
+    closest = h ? tt : closest;
+    face = h ? f : face;
+  };
+  side(hit_rect_inv<2, 0, 1>(o, d, inv, p0.x, p1.x, p0.y, p1.y, p1.z, tmin, closest, tt), 0);
+  side(hit_rect_inv<2, 0, 1>(o, d, inv, p0.x, p1.x, p0.y, p1.y, p0.z, tmin, closest, tt), 1);
+  side(hit_rect_inv<1, 0, 2>(o, d, inv, p0.x, p1.x, p0.z, p1.z, p1.y, tmin, closest, tt), 2);
+  side(hit_rect_inv<1, 0, 2>(o, d, inv, p0.x, p1.x, p0.z, p1.z, p0.y, tmin, closest, tt), 3);
+  side(hit_rect_inv<0, 1, 2>(o, d, inv, p0.y, p1.y, p0.z, p1.z, p1.x, tmin, closest, tt), 4);
+  side(hit_rect_inv<0, 1, 2>(o, d, inv, p0.y, p1.y, p0.z, p1.z, p0.x, tmin, closest, tt), 5);
   t = closest;
   return face;
 }

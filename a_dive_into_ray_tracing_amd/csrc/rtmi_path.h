@@ -546,8 +546,11 @@ __device__ __forceinline__ void resolve_root(int32_t idx, float hb, float disc, 
   const float sq = dsqrt(disc);
   const float r1 = (-hb - sq) * inv_a, r2 = (-hb + sq) * inv_a;
   const bool later = idx > best;
-  const bool ok1 = !(r1 < 0.001f) && (r1 < t_max || (r1 == t_max && later));
-  const bool ok2 = !(r2 < 0.001f) && (r2 < t_max || (r2 == t_max && later));
+  // bitwise, not short-circuit: compare masks combined by scalar ops instead
+  // of nested exec-mask branches (config 2: 23.55 -> 23.25 ms,
+  // profiles/r03/ab_accept.txt)
+  const bool ok1 = !(r1 < 0.001f) & ((r1 < t_max) | ((r1 == t_max) & later));
+  const bool ok2 = !(r2 < 0.001f) & ((r2 < t_max) | ((r2 == t_max) & later));
   if (ok1 || ok2) {
     t_max = ok1 ? r1 : r2;
     best = idx;

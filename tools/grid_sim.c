@@ -1,0 +1,280 @@
+/* tools/grid_sim.c — CPU model of the uniform-grid walk's SIMD efficiency on
+ * the final scene, and of regrouping rays across a block's waves.
+ *
+ * Analysis only (not product, not oracle).  Traces an approximate path
+ * distribution over the fixture scene (as tools/bvh_sim.c: camera rays, then
+ * lambertian / metal / dielectric bounces, brute-force closest hit in double),
+ * records every segment, and replays the segments through the grid walk of
+ * hit_world_grid (big spheres first for t_max, clip to the grid box, 3D DDA,
+ * stop at the first cell whose exit is >= t_max) in 64-lane lockstep groups.
+ * A wave pays for its longest walk: per wave the cell iterations are the max
+ * over lanes of the cells walked, the sphere iterations the sum over cell
+ * steps of the max over lanes of that cell's list length.
+ *
+ * Groupings of a tile's (shuffled) segments into waves:
+ *   shuffled  64 consecutive segments (path regeneration mixes depths: the kernel today)
+ *   block/K   256 consecutive segments (a 4-wave block) sorted by key K, then cut into 4 waves
+ *   ideal/K   all of the tile's segments sorted by key K (an upper bound on any regrouping)
+ * keys: oct = direction octant; cell = entry cell; oct+cell; len = the walk's own cell count (oracle)
+ *
+ *   gcc -O2 -o /tmp/grid_sim tools/grid_sim.c -lm && /tmp/grid_sim tests/golden/scene_final.txt [spp] [stride]
+ */
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define MAXS 1024
+static int N;
+static double C[MAXS][4];
+static int KIND[MAXS];
+static double MAT[MAXS][4];
+
+static unsigned long long rs = 88172645463325252ull;
+static double rnd(void) {
+  rs ^= rs << 13; rs ^= rs >> 7; rs ^= rs << 17;
+  return (rs >> 11) * (1.0 / 9007199254740992.0);
+}
+
+typedef struct { double o[3], d[3]; } Ray;
+static Ray *segs; static int nseg, capseg;
+static int *tile_start; static int ntiles, captiles;
+
+static int hit_bf(const double o[3], const double d[3], double *tt) {
+  double tmax = INFINITY; int best = -1;
+  double a = d[0]*d[0]+d[1]*d[1]+d[2]*d[2];
+  for (int k = 0; k < N; k++) {
+    double oc[3] = {o[0]-C[k][0], o[1]-C[k][1], o[2]-C[k][2]};
+    double hb = oc[0]*d[0]+oc[1]*d[1]+oc[2]*d[2];
+    double c = oc[0]*oc[0]+oc[1]*oc[1]+oc[2]*oc[2]-C[k][3]*C[k][3];
+    double disc = hb*hb - a*c;
+    if (disc < 0) continue;
+    double sq = sqrt(disc), r = (-hb - sq)/a;
+    if (r < 0.001 || r > tmax) { r = (-hb + sq)/a; if (r < 0.001 || r > tmax) continue; }
+    tmax = r; best = k;
+  }
+  *tt = tmax; return best;
+}
+
+static void rand_unit(double v[3]) {
+  double z = 1 - 2*rnd(), ph = 2*M_PI*rnd(), s = sqrt(1 - z*z);
+  v[0] = s*cos(ph); v[1] = s*sin(ph); v[2] = z;
+}
+
+static void push(const double o[3], const double d[3]) {
+  if (nseg == capseg) { capseg = capseg ? 2*capseg : 1<<20; segs = realloc(segs, capseg*sizeof(Ray)); }
+  memcpy(segs[nseg].o, o, 24); memcpy(segs[nseg].d, d, 24); nseg++;
+}
+
+/* ---- grid (build_grid's shape: small spheres, margin-grown boxes, ~0.3 cells per sphere) ---- */
+static int small_[MAXS], nsmall, big_[MAXS], nbig;
+static double g0[3], h[3]; static int n[3];
+static int *cell_start, *cell_refs;
+
+static void build(double density) {
+  double rad[MAXS]; int m = 0;
+  for (int k = 0; k < N; k++) rad[m++] = fabs(C[k][3]);
+  for (int i = 0; i < m; i++) for (int j = i + 1; j < m; j++) if (rad[j] < rad[i]) { double t = rad[i]; rad[i] = rad[j]; rad[j] = t; }
+  double med = rad[m/2];
+  nsmall = nbig = 0;
+  for (int k = 0; k < N; k++) { if (fabs(C[k][3]) > 4*med) big_[nbig++] = k; else small_[nsmall++] = k; }
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int i = 0; i < nsmall; i++) { int k = small_[i]; double r = fabs(C[k][3]) * 1.001 + 1e-6;
+    for (int a = 0; a < 3; a++) { if (C[k][a]-r < lo[a]) lo[a] = C[k][a]-r; if (C[k][a]+r > hi[a]) hi[a] = C[k][a]+r; } }
+  double ext[3], vol = 1; for (int a = 0; a < 3; a++) { ext[a] = hi[a]-lo[a]; vol *= ext[a]; }
+  double side = cbrt(vol / (density * nsmall));
+  int tot = 1;
+  for (int a = 0; a < 3; a++) { n[a] = (int)floor(ext[a]/side + 0.5); if (n[a] < 1) n[a] = 1; if (n[a] > 64) n[a] = 64; g0[a] = lo[a]; h[a] = ext[a]/n[a]; tot *= n[a]; }
+  int *cnt = calloc(tot + 1, sizeof(int));
+  for (int pass = 0; pass < 2; pass++) {
+    for (int i = 0; i < nsmall; i++) { int k = small_[i]; double r = fabs(C[k][3]) * 1.001 + 1e-6; int c0[3], c1[3];
+      for (int a = 0; a < 3; a++) { c0[a] = (int)floor((C[k][a]-r-g0[a])/h[a]); c1[a] = (int)floor((C[k][a]+r-g0[a])/h[a]);
+        if (c0[a] < 0) c0[a] = 0; if (c1[a] >= n[a]) c1[a] = n[a]-1; }
+      for (int z = c0[2]; z <= c1[2]; z++) for (int y = c0[1]; y <= c1[1]; y++) for (int x = c0[0]; x <= c1[0]; x++) {
+        int c = x + n[0]*(y + n[1]*z);
+        if (pass == 0) cnt[c+1]++; else cell_refs[cnt[c]++] = k; } }
+    if (pass == 0) { for (int c = 0; c < tot; c++) cnt[c+1] += cnt[c]; cell_start = malloc((tot+1)*sizeof(int));
+      memcpy(cell_start, cnt, (tot+1)*sizeof(int)); cell_refs = malloc((cnt[tot] + 1)*sizeof(int)); }
+  }
+  printf("grid %d x %d x %d, %d small spheres, %d refs (%.2f per sphere), %d big\n", n[0], n[1], n[2], nsmall,
+         cell_start[tot], (double)cell_start[tot]/nsmall, nbig);
+  free(cnt);
+}
+
+/* one segment's walk: the list lengths of the cells visited (returns their count) */
+static int walk(const Ray *r, int *lens, int *entry_cell) {
+  double a = r->d[0]*r->d[0]+r->d[1]*r->d[1]+r->d[2]*r->d[2], tmax = INFINITY;
+  for (int i = 0; i < nbig; i++) { int q = big_[i];
+    double oc[3] = {r->o[0]-C[q][0], r->o[1]-C[q][1], r->o[2]-C[q][2]};
+    double hb = oc[0]*r->d[0]+oc[1]*r->d[1]+oc[2]*r->d[2];
+    double c = oc[0]*oc[0]+oc[1]*oc[1]+oc[2]*oc[2]-C[q][3]*C[q][3];
+    double disc = hb*hb - a*c; if (disc < 0) continue;
+    double sq = sqrt(disc), rt = (-hb-sq)/a;
+    if (rt < 0.001 || rt > tmax) { rt = (-hb+sq)/a; if (rt < 0.001 || rt > tmax) continue; }
+    tmax = rt; }
+  double inv[3], tn = 0, tf = tmax;
+  for (int k = 0; k < 3; k++) { inv[k] = 1.0 / (fabs(r->d[k]) < 1e-20 ? copysign(1e-20, r->d[k]) : r->d[k]);
+    double t0 = (g0[k]-r->o[k])*inv[k], t1 = (g0[k]+n[k]*h[k]-r->o[k])*inv[k];
+    if (t0 > t1) { double x = t0; t0 = t1; t1 = x; } if (t0 > tn) tn = t0; if (t1 < tf) tf = t1; }
+  *entry_cell = -1;
+  if (tn > tf) return 0;
+  int c[3], step[3]; double tnext[3], dt[3];
+  for (int k = 0; k < 3; k++) { double p = r->o[k] + tn*r->d[k]; c[k] = (int)floor((p-g0[k])/h[k]);
+    if (c[k] < 0) c[k] = 0; if (c[k] >= n[k]) c[k] = n[k]-1;
+    step[k] = r->d[k] >= 0 ? 1 : -1; dt[k] = fabs(h[k]*inv[k]);
+    tnext[k] = (g0[k] + (c[k] + (step[k] > 0)) * h[k] - r->o[k]) * inv[k]; }
+  *entry_cell = c[0] + n[0]*(c[1] + n[1]*c[2]);
+  int nc = 0;
+  for (;;) {
+    int cell = c[0] + n[0]*(c[1] + n[1]*c[2]);
+    lens[nc++] = cell_start[cell+1] - cell_start[cell];
+    /* the spheres tested here can only shrink tmax */
+    for (int i = cell_start[cell]; i < cell_start[cell+1]; i++) { int q = cell_refs[i];
+      double oc[3] = {r->o[0]-C[q][0], r->o[1]-C[q][1], r->o[2]-C[q][2]};
+      double hb = oc[0]*r->d[0]+oc[1]*r->d[1]+oc[2]*r->d[2];
+      double cc = oc[0]*oc[0]+oc[1]*oc[1]+oc[2]*oc[2]-C[q][3]*C[q][3];
+      double disc = hb*hb - a*cc; if (disc < 0) continue;
+      double sq = sqrt(disc), rt = (-hb-sq)/a;
+      if (rt < 0.001 || rt > tmax) { rt = (-hb+sq)/a; if (rt < 0.001 || rt > tmax) continue; }
+      tmax = rt; }
+    int k = tnext[0] <= tnext[1] && tnext[0] <= tnext[2] ? 0 : (tnext[1] <= tnext[2] ? 1 : 2);
+    if (!(tnext[k] < tmax)) break;
+    c[k] += step[k];
+    if (c[k] < 0 || c[k] >= n[k]) break;
+    tnext[k] += dt[k];
+  }
+  return nc;
+}
+
+typedef struct { int nc, oct, cell, lens[128]; } Walk;
+static Walk *W;
+static int key_mode;
+static int key_of(const Walk *w) {
+  switch (key_mode) {
+    case 0: return w->oct;
+    case 1: return w->cell;
+    case 2: return w->oct * 100000 + w->cell + 1;
+    default: return w->nc;
+  }
+}
+static int cmpk(const void *x, const void *y) {
+  int a = key_of(&W[*(const int *)x]), b = key_of(&W[*(const int *)y]);
+  return a < b ? -1 : a > b;
+}
+
+typedef struct { double lane_cells, lane_spheres, wave_cells, wave_spheres, waves; } Acc;
+static void wave_cost(const int *ids, int nl, Acc *acc) {
+  int maxc = 0;
+  for (int l = 0; l < nl; l++) { const Walk *w = &W[ids[l]]; if (w->nc > maxc) maxc = w->nc;
+    acc->lane_cells += w->nc; for (int i = 0; i < w->nc; i++) acc->lane_spheres += w->lens[i]; }
+  acc->wave_cells += maxc;
+  for (int s = 0; s < maxc; s++) { int m = 0; for (int l = 0; l < nl; l++) { const Walk *w = &W[ids[l]]; if (s < w->nc && w->lens[s] > m) m = w->lens[s]; } acc->wave_spheres += m; }
+  acc->waves++;
+}
+
+/* the walk as ONE loop whose iteration is either a cell step or one sphere of
+ * the current cell, per lane (the "if-if" form): iterations where some lane
+ * tests a sphere (ns), where some lane steps a cell (nc), and in total (nt) */
+static double u_ns, u_nc, u_nt;
+static void unified_cost(const int *ids, int nl) {
+  int pos[64] = {0}, cell[64] = {0}, left[64];
+  for (int l = 0; l < nl; l++) left[l] = -1;  /* -1: the next event is a cell step */
+  for (;;) {
+    int any = 0, s = 0, c = 0;
+    for (int l = 0; l < nl; l++) {
+      const Walk *w = &W[ids[l]];
+      if (left[l] > 0) { left[l]--; s = 1; any = 1; continue; }
+      if (cell[l] < w->nc) { left[l] = w->lens[cell[l]]; cell[l]++; c = 1; any = 1; continue; }
+    }
+    (void)pos;
+    if (!any) break;
+    u_ns += s; u_nc += c; u_nt += 1;
+  }
+}
+
+static void report(const char *name, const Acc *a) {
+  printf("  %-14s lane cells %5.3f spheres %5.3f | wave cells %5.3f spheres %6.3f | util cells %.3f spheres %.3f\n", name,
+         a->lane_cells / nseg, a->lane_spheres / nseg, a->wave_cells * 64 / nseg, a->wave_spheres * 64 / nseg,
+         a->lane_cells / (64 * a->wave_cells), a->lane_spheres / (64 * a->wave_spheres));
+}
+
+int main(int argc, char **argv) {
+  FILE *f = fopen(argc > 1 ? argv[1] : "tests/golden/scene_final.txt", "r");
+  if (!f || fscanf(f, "%d", &N) != 1) return 1;
+  for (int k = 0; k < N; k++)
+    if (fscanf(f, "%lf %lf %lf %lf %d %lf %lf %lf %lf", &C[k][0], &C[k][1], &C[k][2], &C[k][3], &KIND[k],
+               &MAT[k][0], &MAT[k][1], &MAT[k][2], &MAT[k][3]) != 9) return 1;
+  double org[3] = {13, 2, 3}, llc[3] = {3.0237371659391918, -1.2262841980681716, 3.4122032022021487},
+         hor[3] = {1.189463936993608, 0, -5.1543437269723009}, ver[3] = {-0.50942050206062017, 3.4875711294919385, -0.11755857739860466},
+         cu[3] = {0.22485950669875845, 0, -0.97439119569461996}, cv[3] = {-0.14445336159384606, 0.98894993706556156, -0.033335391137041398};
+  double lens = 0.05;
+  int Wd = 1200, Ht = 800, spp = argc > 2 ? atoi(argv[2]) : 16, stride = argc > 3 ? atoi(argv[3]) : 7;
+  for (int ty = 0; ty < Ht/8; ty += stride) for (int tx = 0; tx < Wd/8; tx += stride) {
+    if (ntiles + 1 >= captiles) { captiles = captiles ? 2*captiles : 1024; tile_start = realloc(tile_start, captiles*sizeof(int)); }
+    int start = tile_start[ntiles++] = nseg;
+    for (int s = 0; s < spp; s++) for (int p = 0; p < 64; p++) {
+      int i = tx*8 + p%8, j = ty*8 + p/8;
+      double u = (i + rnd())/(Wd-1), v = (j + rnd())/(Ht-1);
+      double rr = sqrt(rnd())*lens, ph = 2*M_PI*rnd(), dx = rr*cos(ph), dy = rr*sin(ph);
+      double o[3], d[3];
+      for (int a = 0; a < 3; a++) { o[a] = org[a] + cu[a]*dx + cv[a]*dy; d[a] = llc[a] + u*hor[a] + v*ver[a] - o[a]; }
+      for (int depth = 0; depth < 50; depth++) {
+        push(o, d);
+        double t; int k = hit_bf(o, d, &t);
+        if (k < 0) break;
+        double pp[3], nn[3], r = C[k][3];
+        for (int a = 0; a < 3; a++) { pp[a] = o[a] + t*d[a]; nn[a] = (pp[a]-C[k][a])/r; }
+        double dn = d[0]*nn[0]+d[1]*nn[1]+d[2]*nn[2];
+        int front = dn < 0; if (!front) for (int a = 0; a < 3; a++) nn[a] = -nn[a];
+        double nd[3], ru[3]; rand_unit(ru);
+        if (KIND[k] == 0) { for (int a = 0; a < 3; a++) nd[a] = nn[a] + ru[a]; }
+        else if (KIND[k] == 1) {
+          double dl = sqrt(d[0]*d[0]+d[1]*d[1]+d[2]*d[2]), ud[3]; for (int a = 0; a < 3; a++) ud[a] = d[a]/dl;
+          double c = ud[0]*nn[0]+ud[1]*nn[1]+ud[2]*nn[2];
+          for (int a = 0; a < 3; a++) nd[a] = ud[a] - 2*c*nn[a] + MAT[k][3]*ru[a]*rnd();
+          if (nd[0]*nn[0]+nd[1]*nn[1]+nd[2]*nn[2] <= 0) break;
+        } else {
+          double dl = sqrt(d[0]*d[0]+d[1]*d[1]+d[2]*d[2]), ud[3]; for (int a = 0; a < 3; a++) ud[a] = d[a]/dl;
+          double eta = front ? 1/1.5 : 1.5, c = -(ud[0]*nn[0]+ud[1]*nn[1]+ud[2]*nn[2]); if (c > 1) c = 1;
+          double s2 = eta*eta*(1-c*c);
+          if (s2 > 1 || rnd() < 0.05) for (int a = 0; a < 3; a++) nd[a] = ud[a] + 2*c*nn[a];
+          else { double k2 = sqrt(1-s2); for (int a = 0; a < 3; a++) nd[a] = eta*ud[a] + (eta*c - k2)*nn[a]; }
+        }
+        double side = nd[0]*nn[0]+nd[1]*nn[1]+nd[2]*nn[2] < 0 ? -1 : 1;
+        for (int a = 0; a < 3; a++) { o[a] = pp[a] + side*7e-4*nn[a]; d[a] = nd[a]; }
+      }
+    }
+    for (int i = nseg - 1; i > start; i--) {  /* path regeneration mixes depths in a wave */
+      int jx = start + (int)(rnd() * (i - start + 1));
+      Ray t = segs[i]; segs[i] = segs[jx]; segs[jx] = t;
+    }
+  }
+  tile_start[ntiles] = nseg;
+  printf("segments %d in %d tiles (%d spp)\n", nseg, ntiles, spp);
+  build(getenv("DENSITY") ? atof(getenv("DENSITY")) : 0.3);
+  W = malloc(nseg * sizeof(Walk));
+  for (int i = 0; i < nseg; i++) {
+    W[i].nc = walk(&segs[i], W[i].lens, &W[i].cell);
+    W[i].oct = (segs[i].d[0] < 0) | ((segs[i].d[1] < 0) << 1) | ((segs[i].d[2] < 0) << 2);
+  }
+  int *ids = malloc(nseg * sizeof(int));
+  Acc a = {0};
+  for (int i = 0; i < nseg; i += 64) { int nl = nseg - i < 64 ? nseg - i : 64; for (int l = 0; l < nl; l++) ids[l] = i + l; wave_cost(ids, nl, &a); }
+  report("shuffled", &a);
+  for (int i = 0; i < nseg; i += 64) { int nl = nseg - i < 64 ? nseg - i : 64; for (int l = 0; l < nl; l++) ids[l] = i + l; unified_cost(ids, nl); }
+  printf("  one loop (if-if): iterations %.3f per wave-segment: with a sphere test %.3f, with a cell step %.3f\n",
+         u_nt * 64 / nseg, u_ns * 64 / nseg, u_nc * 64 / nseg);
+  const char *kn[4] = {"oct", "cell", "oct+cell", "len"};
+  for (int block = 256; block <= 1024; block *= 2)
+    for (key_mode = 0; key_mode < 4; key_mode++) {
+      Acc b = {0};
+      for (int t = 0; t < ntiles; t++) for (int i = tile_start[t]; i < tile_start[t+1]; i += block) {
+        int nb = tile_start[t+1] - i < block ? tile_start[t+1] - i : block;
+        for (int l = 0; l < nb; l++) ids[l] = i + l;
+        qsort(ids, nb, sizeof(int), cmpk);
+        for (int w = 0; w < nb; w += 64) wave_cost(ids + w, nb - w < 64 ? nb - w : 64, &b);
+      }
+      char nm[32]; snprintf(nm, sizeof nm, "%d/%s", block, kn[key_mode]); report(nm, &b);
+    }
+  return 0;
+}

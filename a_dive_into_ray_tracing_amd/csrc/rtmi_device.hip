@@ -1625,7 +1625,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   const int32_t spp1 = spp - tail;
   const int64_t grid_wpb = bvh ? GridShape<true>::waves : GridShape<false>::waves;
   int32_t nch1 = spp1 > 0 ? (spp1 + chunk1 - 1) / chunk1 : 0;
-  if (ctx->chunk <= 0 && !persistent && tail == 0 && spp1 >= grid_wpb) {
+  if (ctx->chunk <= 0 && !persistent && spp1 >= grid_wpb) {
     // automatic grid schedule: exactly a multiple of the block's waves items
     // per tile, so a block's items share a tile and it flushes once
     // (block_flush).  chunk1 = ceil(spp1 / n1) can leave the last items of a
@@ -1637,7 +1637,14 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     nch1 = int32_t(n1);
   }
   chunk2 = std::min(chunk2, std::max(tail, 1));
-  const int32_t nch2 = tail > 0 ? (tail + chunk2 - 1) / chunk2 : 0;
+  int32_t nch2 = tail > 0 ? (tail + chunk2 - 1) / chunk2 : 0;
+  if (ctx->tail_chunk <= 0 && !persistent && tail >= grid_wpb) {
+    // the short-item phase in a multiple of the block's waves items per tile
+    // too, so its blocks also cover one tile each and flush once
+    int64_t n2 = (nch2 + grid_wpb - 1) / grid_wpb * grid_wpb;
+    chunk2 = int32_t((tail + n2 - 1) / n2);
+    nch2 = int32_t(n2);
+  }
   const int64_t items = tiles * (int64_t(nch1) + nch2);
   if (items > int64_t(INT32_MAX) - 8) return set_error(RT_EINVAL, "too many work items");
   RenderArgs a;
@@ -1648,9 +1655,11 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   a.row0 = row0; a.row_step = row_step; a.nrows_valid = nvalid;
   a.tiles_x = tiles_x; a.n_items = int32_t(items);
   a.tiles = int32_t(tiles); a.spp1 = spp1; a.chunk1 = chunk1; a.nch1 = nch1; a.chunk2 = chunk2; a.nch2 = nch2;
-  a.block_flush = !persistent && nch2 == 0 && nch1 % grid_wpb == 0 && ctx->block_flush;
-  a.block_pool = a.block_flush && ctx->block_pool;
-  a.block_owns_tile = a.block_flush && !pass_accum && nch1 == grid_wpb && ctx->block_owns;
+  // block flush: every block's items are of one tile — both phases hold a
+  // multiple of the block's waves items per tile
+  a.block_flush = !persistent && nch1 % grid_wpb == 0 && nch2 % grid_wpb == 0 && ctx->block_flush;
+  a.block_pool = a.block_flush && nch2 == 0 && ctx->block_pool;
+  a.block_owns_tile = a.block_flush && !pass_accum && nch1 == grid_wpb && nch2 == 0 && ctx->block_owns;
   const bool chunked = pass_accum || nch1 + nch2 > 1;
   if (!ctx->probing) {
     const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush + a.block_owns_tile, a.block_pool, persistent ? 1 : 0,

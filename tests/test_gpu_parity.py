@@ -508,6 +508,31 @@ def test_block_flush_same_image(accel, W, H, S, final_world, monkeypatch):
     assert np.array_equal(imgs[0], want)
 
 
+@pytest.mark.parametrize("accel", ["none", "grid"])
+@pytest.mark.parametrize("tail", [5, 40])
+def test_block_flush_with_tail_phase(accel, tail, final_world, final_renderer):
+    """A short-item tail phase with automatic item sizes keeps a multiple of
+    the block's 4 waves items per tile in BOTH phases, so every block still
+    covers one tile and flushes once (through the accumulator: no block owns
+    its tile).  Bit-exact vs the oracle; the schedule is read back."""
+    W, H, S = 40, 24, 130
+    cam = rt.final_camera(W / H)
+    final_renderer.set_accel(accel)
+    final_renderer.set_kernel("grid")
+    final_renderer.set_schedule(0, tail, 0)
+    try:
+        got = final_renderer.render(cam, W, H, S, 50, SEED)
+        sch = final_renderer.last_schedule()
+    finally:
+        final_renderer.set_schedule(0, -1, 0)
+        final_renderer.set_kernel("auto")
+        final_renderer.set_accel("none")
+    assert sch["items_per_tile"] % 4 == 0 and sch["tail_items_per_tile"] % 4 == 0, sch
+    assert sch["tail_items_per_tile"] > 0 and sch["block_flush"] == 1, sch
+    want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("accel", ["none", "bvh", "grid"])
 def test_cost_probe_same_image_and_count(accel, final_world, final_renderer):
     """A render with no cost map of its layout (set_ordering forgets it) runs a

@@ -174,21 +174,10 @@ template <bool BVH> struct GridShape {
   static constexpr int waves = BVH ? RTMI_BVH_WAVES : kWavesPerBlock;
   static constexpr int per_eu = BVH ? RTMI_ACC_PER_EU : RTMI_WAVES_PER_EU;
 };
-// Persistent-kernel block shape for accelerated scenes: 4-wave blocks at 6
-// waves per SIMD (79 VGPRs, no spills; two accumulator slots per wave beside
-// the staged grid, ~23 KB per block).  Config 2 frame / 1/8 strip, grid:
-// 8-wave blocks at 8 waves/SIMD (17 VGPRs spilled) 33.2 / 5.01 ms, 4-wave at
-// 7 waves/SIMD 33.2 / 5.01, 4-wave at 6: 30.9 / 4.72 (profiles/r02/ab_persistent/).
-#ifndef RTMI_PERSIST_ACC_WAVES
-#define RTMI_PERSIST_ACC_WAVES 4
-#endif
-#ifndef RTMI_PERSIST_ACC_PER_EU
-#define RTMI_PERSIST_ACC_PER_EU 6
-#endif
-template <int ACC> struct PersistShape {
-  static constexpr int waves = ACC ? RTMI_PERSIST_ACC_WAVES : kWavesPerBlock;
-  static constexpr int per_eu = ACC ? RTMI_PERSIST_ACC_PER_EU : RTMI_PERSIST_MIN_BLOCKS;
-};
+// The persistent kernel runs brute-force scenes only: with the BVH or the
+// grid it measured slower than the grid kernel everywhere (round 2: config 2
+// frame / 1/8 strip 30.9 / 4.72 ms against 26.0 / 3.70, profiles/r02/ab_persistent/),
+// so RT_KERNEL_PERSISTENT with an accelerator runs the grid kernel.
 
 // The camera and the reciprocals of main.cpp:278-279's (W-1, H-1)
 // denominators in LDS (21 floats), read at each regeneration instead of held
@@ -578,12 +567,12 @@ __device__ __forceinline__ ItemDesc describe_item(const RenderArgs &a, int item)
   return r;
 }
 
-template <int TW, bool CHUNKED, int ACC>
-__global__ __launch_bounds__(64 * PersistShape<ACC>::waves, PersistShape<ACC>::per_eu) void render_persistent(
+template <int TW, bool CHUNKED>
+__global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void render_persistent(
     const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1,
     const SpherePair *__restrict__ pairs, RenderArgs a, unsigned long long *__restrict__ accum,
     float *__restrict__ out, unsigned long long *__restrict__ segments, unsigned *__restrict__ counter) {
-  constexpr int WPB = PersistShape<ACC>::waves;
+  constexpr int WPB = kWavesPerBlock;
   __shared__ unsigned long long acc[WPB][2][3][64];
   __shared__ unsigned long long wave_segs[WPB];
   __shared__ unsigned slot_segs[WPB][2];  // world.hit calls of each slot's item (tile cost)
@@ -595,9 +584,7 @@ __global__ __launch_bounds__(64 * PersistShape<ACC>::waves, PersistShape<ACC>::p
   const int lane = threadIdx.x & 63;
   __shared__ float cam_lds[21];
   stage_camera(cam_lds, a);
-  if constexpr (ACC == 0) __syncthreads();  // (accelerated kernels: stage_* ends with one)
-  if constexpr (ACC == 1) stage_bvh(a.acc);
-  else if constexpr (ACC >= 2) stage_grid(a.acc);
+  __syncthreads();
   if (lane < 2) slot_segs[wave][lane] = 0;
   for (int s = 0; s < 2; ++s)
     for (int c = 0; c < 3; ++c) acc[wave][s][c][lane] = 0;
@@ -732,7 +719,7 @@ __global__ __launch_bounds__(64 * PersistShape<ACC>::waves, PersistShape<ACC>::p
     V3<float> col = mk(0.f, 0.f, 0.f);
     if (active) {
       ++nseg;
-      done = path_segment<ACC>(sc, pairs, a, o, d, T, depth, rng, col, cnt, segments);
+      done = path_segment<0>(sc, pairs, a, o, d, T, depth, rng, col, cnt, segments);
     }
     // 3. finished paths add their colour to their item's slot
 #if RTMI_CHECK
@@ -913,7 +900,6 @@ struct rt_ctx {
   float4 *bvh_sph = nullptr;
   int32_t *bvh_idx = nullptr;
   int32_t nbvh_sph = 0;
-  int32_t resident_blocks_bvh = 0;  // persistent grid with the BVH's LDS
   // uniform grid, built by rt_ctx_set_scene beside the BVH
   float4 *grid_sph = nullptr;  // every sphere by scene index
   uint32_t *grid_cells = nullptr;  // ncells + 1: each cell's first reference
@@ -921,7 +907,6 @@ struct rt_ctx {
   GridDesc grid{};
   int32_t ngrid_sph = 0;
   bool grid_ok = false;
-  int32_t resident_blocks_grid = 0;
   // cost-ordered dispatch: per-tile world.hit counts of the
   // last render with the same tile layout order the next one's tiles
   int32_t ordering = RT_ORDER_COST;
@@ -1046,7 +1031,7 @@ RTMI_EXPORT int rt_ctx_create(int32_t device, rt_ctx **out) {
     // resident blocks per CU for the persistent grid; over-subscription is
     // harmless (extra waves start later and find the counter exhausted)
     int per_cu = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<8, true, false>,
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<8, true>,
                                                          64 * kWavesPerBlock, 0));
     ctx->resident_blocks = std::max(1, per_cu) * prop.multiProcessorCount;
   }
@@ -1391,13 +1376,6 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
     // offered (RT_ACCEL_BVH renders brute force)
     const size_t lds = bvh_lds_bytes(int32_t(b.nodes.size()), int32_t(b.sph.size()));
     ctx->nnodes = lds <= kBvhLdsMax && n <= 65535 ? int32_t(b.nodes.size()) : 0;
-    int per_cu = 0;
-    if (ctx->nnodes)
-      HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<8, true, 1>,
-                                                           64 * PersistShape<1>::waves, lds));
-    int cus = 0;
-    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    ctx->resident_blocks_bvh = std::max(1, per_cu) * cus;
     // uniform grid over the same small spheres
     ctx->grid_ok = false;
     GridBuild gb;
@@ -1414,11 +1392,6 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
       ctx->grid.refs = ctx->grid_refs;
       ctx->ngrid_sph = int32_t(gb.sph.size());
       ctx->grid_ok = true;
-      const size_t glds = grid_lds_bytes(ctx->ngrid_sph, ctx->grid.ncells, ctx->grid.nrefs);
-      per_cu = 0;
-      HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<8, true, 2>,
-                                                           64 * PersistShape<2>::waves, glds));
-      ctx->resident_blocks_grid = std::max(1, per_cu) * cus;
     }
   }
   ctx->n = n;
@@ -1499,16 +1472,15 @@ Accel accel_of(const rt_ctx *ctx, int kind) {
   return a;
 }
 
-template <int TW, int ACC>
+template <int TW>
 void launch_persistent(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a,
                        unsigned long long *accum, float *out) {
-  const size_t lds = accel_lds_bytes(a.acc, ACC);
   if (chunked)
-    hipLaunchKernelGGL((render_persistent<TW, true, ACC>), grid, dim3(64 * PersistShape<ACC>::waves), lds, st, ctx->geom, ctx->sh0,
+    hipLaunchKernelGGL((render_persistent<TW, true>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
                        ctx->sh1, ctx->pairs, a, accum, out, ctx->segments, ctx->counter);
   else
-    hipLaunchKernelGGL((render_persistent<TW, false, ACC>), grid, dim3(64 * PersistShape<ACC>::waves), lds, st, ctx->geom,
-                       ctx->sh0, ctx->sh1, ctx->pairs, a, accum, out, ctx->segments, ctx->counter);
+    hipLaunchKernelGGL((render_persistent<TW, false>), grid, dim3(64 * kWavesPerBlock), 0, st, ctx->geom, ctx->sh0,
+                       ctx->sh1, ctx->pairs, a, accum, out, ctx->segments, ctx->counter);
 }
 
 template <int TW, int ACC>
@@ -1526,10 +1498,8 @@ void launch_tw(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const
 template <int TW>
 void launch_shape(bool persistent, int acc, bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx,
                   const RenderArgs &a, unsigned long long *accum, float *out) {
-  if (persistent) {
-    if (acc == 1) launch_persistent<TW, 1>(chunked, grid, st, ctx, a, accum, out);
-    else if (acc >= 2) launch_persistent<TW, 2>(chunked, grid, st, ctx, a, accum, out);  // (the general walk)
-    else launch_persistent<TW, 0>(chunked, grid, st, ctx, a, accum, out);
+  if (persistent) {  // brute force only
+    launch_persistent<TW>(chunked, grid, st, ctx, a, accum, out);
   } else {
     if (acc == 1) launch_tw<TW, 1>(chunked, grid, st, ctx, a, accum, out);
     else if (acc == 2) launch_tw<TW, 2>(chunked, grid, st, ctx, a, accum, out);
@@ -1586,22 +1556,16 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   // has one; both stage their structure in LDS and use the same block shape
   // (3: the grid has one cell layer in y and the grid kernel walks it with
   // the y stepping dropped, hit_world_grid<.., true>: the same cells, 3% faster
-  // on config 2; the persistent kernel keeps the general walk)
+  // on config 2)
   const int acc_kind = ctx->accel == RT_ACCEL_BVH && ctx->nnodes > 0
                            ? 1
                            : (ctx->accel == RT_ACCEL_GRID && ctx->grid_ok ? (ctx->grid.n[1] == 1 ? 3 : 2) : 0);
   const bool bvh = acc_kind != 0;
-  const bool persistent = ctx->kernel == RT_KERNEL_PERSISTENT ||
-                          (ctx->kernel == RT_KERNEL_AUTO && !bvh && tile_samples < 6000000);
+  // the persistent kernel runs brute-force scenes only (see the note above stage_camera)
+  const bool persistent = !bvh && (ctx->kernel == RT_KERNEL_PERSISTENT ||
+                                   (ctx->kernel == RT_KERNEL_AUTO && tile_samples < 6000000));
   int32_t chunk1 = ctx->chunk, chunk2 = ctx->tail_chunk, tail = ctx->tail_spp;
-  if (chunk1 <= 0 && persistent && bvh) {
-    // accelerated scenes: ~8 items per resident wave, 8..32 samples (grid,
-    // 1/8 strip: chunk 8 -> 4.41 ms, 16 -> 4.27, 32 -> 4.43, 64 -> 6.69; frame
-    // 31.0-32.9 for 8..64; profiles/r02/ab_persistent/pers_chunk)
-    const int64_t waves = int64_t(acc_kind == 1 ? ctx->resident_blocks_bvh : ctx->resident_blocks_grid) *
-                          (acc_kind == 1 ? PersistShape<1>::waves : PersistShape<2>::waves);  // (2 and 3)
-    chunk1 = int32_t(std::min<int64_t>(32, std::max<int64_t>(8, tile_samples / (8 * waves))));
-  } else if (chunk1 <= 0 && persistent) {
+  if (chunk1 <= 0 && persistent) {
     // ~28 items per resident wave (1/8 strip: chunk 8 -> 17.5 ms, 16 -> 17.9, 32 -> 19.7)
     const int64_t waves = int64_t(ctx->resident_blocks) * kWavesPerBlock;
     chunk1 = int32_t(std::min<int64_t>(64, std::max<int64_t>(4, tile_samples / (28 * waves))));
@@ -1750,11 +1714,8 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   if (persistent) {
     // a resident grid of waves pulling items from a global counter
     HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
-    const int64_t pw = acc_kind == 1 ? PersistShape<1>::waves : acc_kind >= 2 ? PersistShape<2>::waves
-                                                                                : PersistShape<0>::waves;
-    const int64_t waves =
-        std::min<int64_t>(items, int64_t(acc_kind == 1 ? ctx->resident_blocks_bvh
-                                         : acc_kind >= 2 ? ctx->resident_blocks_grid : ctx->resident_blocks) * pw);
+    const int64_t pw = kWavesPerBlock;
+    const int64_t waves = std::min<int64_t>(items, int64_t(ctx->resident_blocks) * pw);
     grid = dim3(unsigned((waves + pw - 1) / pw));
   } else {
     const int64_t wpb = bvh ? GridShape<true>::waves : GridShape<false>::waves;

@@ -134,10 +134,11 @@ int rt_ctx_set_schedule(rt_ctx *ctx, int32_t chunk, int32_t tail_spp, int32_t ta
 
 /* Kernel shape.  RT_KERNEL_PERSISTENT: a resident grid of waves pulls work
  * items from a global counter and streams paths continuously (two items in
- * flight per wave).  RT_KERNEL_GRID: one wave per work item.
- * RT_KERNEL_AUTO (default): persistent for brute-force strips (RT_ACCEL_NONE
- * and fewer than 6e6 tile-samples), grid otherwise — the grid and BVH
- * accelerators always take RT_KERNEL_GRID.  All give bit-identical images. */
+ * flight per wave) — brute force (RT_ACCEL_NONE) only: with the grid or the
+ * BVH the grid kernel runs, which measured faster.
+ * RT_KERNEL_GRID: one wave per work item.  RT_KERNEL_AUTO (default):
+ * persistent for brute-force strips (fewer than 6e6 tile-samples), grid
+ * otherwise.  All give bit-identical images. */
 enum { RT_KERNEL_GRID = 0, RT_KERNEL_PERSISTENT = 1, RT_KERNEL_AUTO = 2 };
 int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind);
 

@@ -192,6 +192,51 @@ static void unified_cost(const int *ids, int nl) {
   }
 }
 
+
+/* Early-exit walks: per pass, lanes without a walk start one (segment setup:
+ * big spheres + clip), the walk loop runs while more than `thr` lanes are
+ * still walking (a lane's walk state survives the pass), then the lanes whose
+ * walk ended are shaded.  Cost per pass from the kernel's phase split
+ * (per wave-segment, round 3): setup 0.17, shading + regeneration 0.49 when
+ * any lane needs it, a cell iteration 0.0265 and a sphere iteration 0.0204
+ * (3.76 x 0.0265 + 10.78 x 0.0204 = the walk's 0.32).  Lanes draw segments
+ * from the shuffled stream; returns cost per segment relative to thr = 0. */
+static double early_exit(int thr) {
+  const double S = 0.17, R = 0.49, CC = 0.0265, CS = 0.0204;
+  double cost = 0, segs_done = 0;
+  for (int w0 = 0; w0 + 64 * 64 <= nseg; w0 += 64 * 64) {   /* one wave: 64 lanes, 64 segments each */
+    int next[64], cell[64], left[64], walking[64], done_n[64];
+    for (int l = 0; l < 64; l++) { next[l] = w0 + l * 64; done_n[l] = 0; walking[l] = 0; cell[l] = 0; left[l] = 0; }
+    int live = 64;
+    while (live) {
+      /* setup for lanes without a walk */
+      int any_setup = 0;
+      for (int l = 0; l < 64; l++) if (!walking[l] && done_n[l] < 64) { walking[l] = 1; cell[l] = 0; left[l] = -1; any_setup = 1; }
+      if (any_setup) cost += S;
+      /* walk loop: lockstep cell steps (each a cell iteration, then that cell's spheres) */
+      for (;;) {
+        int nwalk = 0;
+        for (int l = 0; l < 64; l++) if (walking[l] && done_n[l] < 64) {
+          const Walk *w = &W[next[l]];
+          if (cell[l] < w->nc) nwalk++; }
+        if (nwalk == 0 || (nwalk <= thr && nwalk < live)) break;
+        int maxlen = 0;
+        for (int l = 0; l < 64; l++) if (walking[l] && done_n[l] < 64) {
+          const Walk *w = &W[next[l]];
+          if (cell[l] < w->nc) { if (w->lens[cell[l]] > maxlen) maxlen = w->lens[cell[l]]; cell[l]++; } }
+        cost += CC + maxlen * CS;
+      }
+      /* shade the lanes whose walk ended */
+      int any_ready = 0;
+      for (int l = 0; l < 64; l++) if (walking[l] && done_n[l] < 64) {
+        const Walk *w = &W[next[l]];
+        if (cell[l] >= w->nc) { walking[l] = 0; next[l]++; done_n[l]++; segs_done++; any_ready = 1; if (done_n[l] == 64) live--; } }
+      if (any_ready) cost += R;
+    }
+  }
+  return cost * 64 / segs_done;   /* per wave-segment, as the phase split */
+}
+
 static void report(const char *name, const Acc *a) {
   printf("  %-14s lane cells %5.3f spheres %5.3f | wave cells %5.3f spheres %6.3f | util cells %.3f spheres %.3f\n", name,
          a->lane_cells / nseg, a->lane_spheres / nseg, a->wave_cells * 64 / nseg, a->wave_spheres * 64 / nseg,
@@ -264,6 +309,12 @@ int main(int argc, char **argv) {
   for (int i = 0; i < nseg; i += 64) { int nl = nseg - i < 64 ? nseg - i : 64; for (int l = 0; l < nl; l++) ids[l] = i + l; unified_cost(ids, nl); }
   printf("  one loop (if-if): iterations %.3f per wave-segment: with a sphere test %.3f, with a cell step %.3f\n",
          u_nt * 64 / nseg, u_ns * 64 / nseg, u_nc * 64 / nseg);
+  {
+    const double base = early_exit(0);
+    printf("  early-exit walks (cost per wave-segment, thr 0 = the kernel today = %.3f):", base);
+    for (int thr = 1; thr <= 32; thr *= 2) printf("  thr %d: %.3f", thr, early_exit(thr) / base);
+    printf("\n");
+  }
   const char *kn[4] = {"oct", "cell", "oct+cell", "len"};
   for (int block = 256; block <= 1024; block *= 2)
     for (key_mode = 0; key_mode < 4; key_mode++) {

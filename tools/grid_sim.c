@@ -202,7 +202,8 @@ static void unified_cost(const int *ids, int nl) {
  * (3.76 x 0.0265 + 10.78 x 0.0204 = the walk's 0.32).  Lanes draw segments
  * from the shuffled stream; returns cost per segment relative to thr = 0. */
 static double early_exit(int thr) {
-  const double S = 0.17, R = 0.49, CC = 0.0265, CS = 0.0204;
+  const double S = getenv("SIM_S") ? atof(getenv("SIM_S")) : 0.17, R = getenv("SIM_R") ? atof(getenv("SIM_R")) : 0.49;
+  const double wk = getenv("SIM_W") ? atof(getenv("SIM_W")) / 0.32 : 1.0, CC = 0.0265 * wk, CS = 0.0204 * wk;
   double cost = 0, segs_done = 0;
   for (int w0 = 0; w0 + 64 * 64 <= nseg; w0 += 64 * 64) {   /* one wave: 64 lanes, 64 segments each */
     int next[64], cell[64], left[64], walking[64], done_n[64];

@@ -442,6 +442,64 @@ def test_bvh_adversarial_rays_equal_brute_force(accel, final_world):
     assert np.array_equal(t[:, 0], t[:, 1])
 
 
+def test_grid_general_and_one_layer_walks(final_world):
+    """The grid kernel has two walks: the one-layer walk for
+    grids with a single cell layer in y (the final scene: asserted) and the
+    general 3D walk (a scene of spheres filling a cube: asserted ny > 1).
+    For the 3D scene, 200 k adversarial rays through rt_ctx_debug_hits (the
+    walk the renders use) give the brute-force loop's index and t, and a
+    render equals the brute-force render bit for bit."""
+    r = rt.Renderer(final_world, 0)
+    try:
+        r.set_accel("grid")
+        assert r.grid_info()[0][1] == 1
+    finally:
+        r.close()
+    g = np.random.default_rng(5)
+    n = 400
+    c = g.uniform(-4, 4, (n, 3))
+    rad = np.exp(g.uniform(np.log(0.05), np.log(0.4), n))
+    kinds = g.integers(0, 3, n).astype(np.int32)
+    params = np.column_stack([g.uniform(0.1, 0.9, (n, 3)), np.where(kinds == 2, 1.5, g.uniform(0, 0.5, n))])
+    cr = np.vstack([[0, -1000, 0, 1000], np.column_stack([c, rad])])
+    kinds = np.concatenate([[0], kinds]).astype(np.int32)
+    params = np.vstack([[0.5, 0.5, 0.5, 0], params])
+    world = rt.World(cr, kinds, params)
+    cam = rt.camera((13, 2, 3), (0, 0, 0), (0, 1, 0), 40.0, 1.5, 0.1, 10.0)
+    r = rt.Renderer(world, 0)
+    L = rt.load()
+    L.rt_ctx_debug_hits.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_float)]
+    try:
+        r.set_accel("none")
+        want = r.render(cam, 64, 48, 6, 50, SEED)
+        r.set_accel("grid")
+        dims = r.grid_info()[0]
+        assert dims[1] > 1, dims
+        got = r.render(cam, 64, 48, 6, 50, SEED)
+        assert r.last_schedule()["bvh"] == 2
+        m = 200_000
+        o = g.uniform(-5, 5, (m, 3))
+        k = g.integers(1, n + 1, m // 2)
+        u = g.normal(size=(m // 2, 3))
+        u /= np.linalg.norm(u, axis=1, keepdims=True)
+        o[: m // 2] = cr[k, :3] + u * (cr[k, 3:4] * (1 + g.choice([1e-3, 1e-4, -1e-4, 0.0], m // 2)[:, None]))
+        dv = g.normal(size=(m, 3))
+        dv[g.random((m, 3)) < 0.03] = 0.0
+        dv[np.all(dv == 0, axis=1)] = [0, -1, 0]
+        rays = np.ascontiguousarray(np.column_stack([o, dv]).astype(np.float32))
+        idx = np.zeros(2 * m, np.int32)
+        t = np.zeros(2 * m, np.float32)
+        rc = L.rt_ctx_debug_hits(r._h, rays.ctypes.data_as(C.POINTER(C.c_float)), m, idx.ctypes.data_as(C.POINTER(C.c_int32)),
+                                 t.ctypes.data_as(C.POINTER(C.c_float)))
+    finally:
+        r.close()
+    assert rc == 0
+    assert np.array_equal(got, want)
+    idx, t = idx.reshape(m, 2), t.reshape(m, 2)
+    assert (idx[:, 0] >= 0).mean() > 0.3
+    assert np.array_equal(idx[:, 0], idx[:, 1]) and np.array_equal(t[:, 0], t[:, 1])
+
+
 @pytest.mark.parametrize("kernel,accel", [("grid", "none"), ("persistent", "none"), ("grid", "bvh"), ("persistent", "bvh"),
                                           ("grid", "grid"), ("persistent", "grid")])
 def test_cost_ordered_dispatch_same_image(kernel, accel, final_world, final_renderer):

@@ -236,7 +236,7 @@ class Renderer:
         """Diagnostic: the last launch's schedule as a dict (rt_ctx_last_schedule)."""
         v = (C.c_int32 * 8)()
         check(self.L.rt_ctx_last_schedule(self._h, v), "rt_ctx_last_schedule")
-        keys = ("tile_w", "chunk", "items_per_tile", "tail_items_per_tile", "block_flush", "block_pool", "persistent", "bvh")
+        keys = ("tile_w", "chunk", "items_per_tile", "tail_items_per_tile", "block_flush", "ray_pool", "persistent", "bvh")
         return dict(zip(keys, list(v)))
 
     def synchronize(self):

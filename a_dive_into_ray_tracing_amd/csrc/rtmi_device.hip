@@ -64,11 +64,6 @@ struct RenderArgs {
   // block's waves, no phase 2), so the block sums its waves' accumulators and
   // flushes once (a quarter of the global atomics)
   int32_t block_flush;
-  // block_flush launches only: the block's waves draw (pixel, sample) jobs
-  // from ONE pool covering their 4 items (an LDS counter), so they drain
-  // together instead of each wave ramping down alone (same image: the
-  // accumulators are fixed point, their sums independent of who adds)
-  int32_t block_pool;
   // block_flush launches whose block covers ALL samples of its tile (items
   // per tile == waves per block, not a progressive pass): the block writes the
   // tile's float sums straight to the output strip — no accumulator memset,
@@ -127,6 +122,12 @@ __device__ unsigned g_trace_n;
 #ifndef RTMI_CHECK
 #define RTMI_CHECK 0
 #endif
+// render_kernel's camera-ray pool; 0: each lane generates
+// its next camera ray itself when its path ends (analysis / A-B builds)
+#ifndef RTMI_RAY_POOL
+#define RTMI_RAY_POOL 1
+#endif
+constexpr int kRayPool = RTMI_RAY_POOL;
 #ifndef RTMI_PERSIST_MIN_BLOCKS
 #define RTMI_PERSIST_MIN_BLOCKS 1
 #endif
@@ -345,18 +346,14 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   constexpr int WPB = GridShape<ACC != 0>::waves;
   __shared__ unsigned long long acc[WPB][3][64];
   __shared__ unsigned long long wave_segs[WPB];
-  __shared__ unsigned pool_next;  // block pool: next unclaimed job
   __shared__ float cam_lds[21];  // the camera (stage_camera)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * WPB + wave;
-  const bool pool = CHUNKED && a.block_pool;  // block-uniform (implies block_flush)
-  if (pool && threadIdx.x == 0) pool_next = 64 * WPB;
   stage_camera(cam_lds, a);
   if constexpr (ACC == 0) __syncthreads();  // (accelerated kernels: stage_* ends with one)
   if constexpr (ACC == 1) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
   else if constexpr (ACC >= 2) stage_grid(a.acc);
-  else if (pool) __syncthreads();
   if (item >= a.n_items) return;  // wave-uniform; no block barrier follows
 
   int tile, s0, ns;
@@ -375,17 +372,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   const int x0 = tx * TW, y0 = ty * TH;
   const int vw = min(TW, a.W - x0), vh = min(TH, a.nrows_valid - y0);
   const int nv = vw * vh;  // valid pixels of this tile
-  int nq = nv * ns;  // jobs: (pixel, sample) pairs of this item
-  int q0 = lane;     // this lane's first job
-  if (pool) {
-    // the block's WPB items are consecutive sample ranges of one tile
-    // (block_flush schedule): one job range [s0 of the first item, its end)
-    const int sb0 = (int(blockIdx.x) * WPB % a.nch1) * a.chunk1;
-    const int sb1 = min(sb0 + WPB * a.chunk1, a.spp1);
-    s0 = sb0;
-    nq = nv * max(sb1 - sb0, 0);
-    q0 = wave * 64 + lane;
-  }
+  const int nq = nv * ns;  // jobs: (pixel, sample) pairs of this item
 
   acc[wave][0][lane] = 0;
   acc[wave][1][lane] = 0;
@@ -402,6 +389,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
 
   V3<float> o, d, T;
   int px = 0, depth = 0;
+  bool active = true;
   Xoro rng;
 
   // job q -> pixel px = q % nv, sample s0 + q / nv (sample-major, so every
@@ -409,27 +397,64 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   // q / nv and px / vw by a float reciprocal with one correction step:
   // exact for q < 2^22 (a job index here is < 64 * spp per item)
   const float inv_nv = 1.0f / float(max(nv, 1)), inv_vw = 1.0f / float(vw);
-  auto start = [&](int q) {
+  auto camera_ray = [&](int q, V3<float> &ro, V3<float> &rd, Xoro &g) {
     const int qs = div_small(q, nv, inv_nv);
     const int s = s0 + qs;
-    px = q - qs * nv;
-    const int ly = div_small(px, vw, inv_vw), lx = px - ly * vw;
+    const int p = q - qs * nv;
+    const int ly = div_small(p, vw, inv_vw), lx = p - ly * vw;
     const int i = x0 + lx;
     const int j = a.row0 + (y0 + ly) * a.row_step;
-    rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(a.s_base + s));
+    g.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(a.s_base + s));
     float ju, jv;
-    rng.pair(ju, jv);
+    g.pair(ju, jv);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // camera read here, not hoisted out of the loop
     const float u = (float(i) + ju) * cam_lds[19];  // main.cpp:278, by the reciprocal
     const float v = (float(j) + jv) * cam_lds[20];  // main.cpp:279
-    get_ray<true, float>(lds_camera(cam_lds), u, v, rng, o, d);
-    T = mk(1.f, 1.f, 1.f);
-    depth = 0;
+    get_ray<true, float>(lds_camera(cam_lds), u, v, g, ro, rd);
+  };
+  // a lane takes job q with its camera ray (or goes idle when the item has
+  // no job q)
+  auto adopt = [&](int q, const V3<float> &ro, const V3<float> &rd, const Xoro &g) {
+    if (q < nq) {
+      o = ro;
+      d = rd;
+      rng = g;
+      px = q - div_small(q, nv, inv_nv) * nv;
+      T = mk(1.f, 1.f, 1.f);
+      depth = 0;
+    } else {
+      active = false;
+    }
   };
 
-  bool active = q0 < nq;
-  if (active) start(q0);
+#if RTMI_RAY_POOL
+  // Camera-ray pool: lane L holds the camera ray of job
+  // pbase + L, generated by all 64 lanes at once; a lane whose path ended
+  // takes the next unused slot through ds_bpermute.  The ray generation runs
+  // with every lane busy, once per 64 jobs, instead of once per loop pass
+  // for the few lanes that regenerate.  Same rays bit for bit.
+  V3<float> po, pd;
+  Xoro prng;
+  int pbase = 0, ppos = 64;  // wave-uniform: job of slot 0, next unused slot
+  camera_ray(lane, po, pd, prng);
+  adopt(lane, po, pd, prng);
+  auto pull = [](int src4, float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(src4, __float_as_int(v))); };
+  auto pull64 = [](int src4, uint64_t v) {
+    const uint32_t lo = uint32_t(__builtin_amdgcn_ds_bpermute(src4, int(uint32_t(v))));
+    const uint32_t hi = uint32_t(__builtin_amdgcn_ds_bpermute(src4, int(uint32_t(v >> 32))));
+    return (uint64_t(hi) << 32) | lo;
+  };
+#else
+  if (lane < nq) {
+    V3<float> ro, rd;
+    Xoro g;
+    camera_ray(lane, ro, rd, g);
+    adopt(lane, ro, rd, g);
+  } else {
+    active = false;
+  }
   int next = 64;
+#endif
 
   for (;;) {
     if (__ballot(active) == 0) break;
@@ -445,25 +470,54 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
 #if RTMI_TRACE_PHASES
     const unsigned long long cyc_b = __builtin_amdgcn_s_memtime();
     cyc_iter += cyc_b - cyc_a;  // hit + shading of this pass (wave-level)
-    const bool ramp = next >= nq;  // the item's jobs all taken: the wave's ramp-down
+#if RTMI_RAY_POOL
+    const bool ramp = pbase + 64 >= nq && ppos == 64;  // the item's jobs all taken: the wave's ramp-down
+#else
+    const bool ramp = next >= nq;
+#endif
 #endif
     const unsigned long long m = __ballot(done);
     if (m) {
-      if (pool) {  // claim popcount(m) jobs of the block pool (one LDS atomic)
-        unsigned b = 0;
-        if (lane == 0) b = atomicAdd(&pool_next, unsigned(__popcll(m)));
-        next = __builtin_amdgcn_readlane(int(b), 0);
-      }
       if (done) {
         atomicAdd(&acc[wave][0][px], (unsigned long long)to_fixed(col.x));
         atomicAdd(&acc[wave][1][px], (unsigned long long)to_fixed(col.y));
         atomicAdd(&acc[wave][2][px], (unsigned long long)to_fixed(col.z));
-        const int rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
+      }
+      const int rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
+#if RTMI_RAY_POOL
+      // ranks [0, cnt) take slots ppos, ppos + 1, ...: at most two rounds,
+      // the second after a refill for the next 64 jobs (skipped once the
+      // item has none: those lanes go idle)
+      const int cnt = __popcll(m);
+      for (int served = 0; served < cnt;) {
+        if (ppos == 64) {
+          pbase += 64;
+          ppos = 0;
+          if (pbase < nq) camera_ray(pbase + lane, po, pd, prng);
+        }
+        const int take = min(cnt - served, 64 - ppos);
+        const int r = rank - served;
+        const int src4 = ((ppos + r) & 63) << 2;  // every lane reads (ds_bpermute reads active lanes only)
+        V3<float> ro, rd;
+        Xoro g;
+        ro = mk(pull(src4, po.x), pull(src4, po.y), pull(src4, po.z));
+        rd = mk(pull(src4, pd.x), pull(src4, pd.y), pull(src4, pd.z));
+        g.s0 = pull64(src4, prng.s0);
+        g.s1 = pull64(src4, prng.s1);
+        if (done && r >= 0 && r < take) adopt(pbase + ppos + r, ro, rd, g);
+        ppos += take;
+        served += take;
+      }
+#else
+      if (done) {
         const int q = next + rank;
-        if (q < nq) start(q);
-        else active = false;
+        V3<float> ro, rd;
+        Xoro g;
+        if (q < nq) camera_ray(q, ro, rd, g);
+        adopt(q, ro, rd, g);
       }
       next += __popcll(m);
+#endif
     }
 #if RTMI_TRACE_PHASES
     const unsigned long long cyc_e = __builtin_amdgcn_s_memtime();
@@ -913,9 +967,6 @@ struct rt_ctx {
   // block-level accumulator flush of the automatic grid schedule (same image;
   // RTMI_BLOCK_FLUSH=0 in the environment turns it off, for A/B and tests)
   bool block_flush = !(std::getenv("RTMI_BLOCK_FLUSH") && std::getenv("RTMI_BLOCK_FLUSH")[0] == '0');
-  // block-shared job pool of block_flush launches (same image; measured
-  // neutral, DESIGN.md §5, so off unless RTMI_BLOCK_POOL=1)
-  bool block_pool = std::getenv("RTMI_BLOCK_POOL") && std::getenv("RTMI_BLOCK_POOL")[0] == '1';
   // a block that covers all samples of its tile writes the floats itself
   // (RTMI_BLOCK_OWNS=0 routes it through the accumulator, for A/B and tests)
   bool block_owns = !(std::getenv("RTMI_BLOCK_OWNS") && std::getenv("RTMI_BLOCK_OWNS")[0] == '0');
@@ -1622,11 +1673,10 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   // block flush: every block's items are of one tile — both phases hold a
   // multiple of the block's waves items per tile
   a.block_flush = !persistent && nch1 % grid_wpb == 0 && nch2 % grid_wpb == 0 && ctx->block_flush;
-  a.block_pool = a.block_flush && nch2 == 0 && ctx->block_pool;
   a.block_owns_tile = a.block_flush && !pass_accum && nch1 == grid_wpb && nch2 == 0 && ctx->block_owns;
   const bool chunked = pass_accum || nch1 + nch2 > 1;
   if (!ctx->probing) {
-    const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush + a.block_owns_tile, a.block_pool, persistent ? 1 : 0,
+    const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush + a.block_owns_tile, persistent ? 0 : kRayPool, persistent ? 1 : 0,
                               acc_kind == 3 ? 2 : acc_kind};
     std::copy(sched, sched + 8, ctx->last_sched);
   }

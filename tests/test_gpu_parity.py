@@ -532,18 +532,15 @@ def test_block_flush_same_image(accel, W, H, S, final_world, monkeypatch):
     """The automatic grid schedule gives every block exactly 4 items of one
     tile and flushes the block's summed accumulators once — here the block
     owns its tile and writes the floats itself (RTMI_BLOCK_OWNS=0: through
-    the accumulator).  RTMI_BLOCK_POOL=1 makes the block's waves draw
-    (pixel, sample) jobs from one block-wide pool; RTMI_BLOCK_FLUSH=0 flushes
-    per wave.  Same image and world.hit count
+    the accumulator); RTMI_BLOCK_FLUSH=0 flushes per wave.  Same image and world.hit count
     bit for bit, equal to the oracle.  37 spp: items of 10/10/10/7 samples;
     29x19: partial tiles (automatic 16x4 shape); 29x19 at 5 spp: items of
     2/2/1/0 samples (the empty item's wave only joins the flush).  The launch
     schedule is read back, so the test cannot pass on a path it skipped."""
     cam = rt.final_camera(W / H)
     imgs, segs = [], []
-    for flush, pool, owns in (("1", "1", "1"), ("1", "0", "1"), ("0", "1", "1"), ("1", "0", "0")):
+    for flush, owns in (("1", "1"), ("0", "1"), ("1", "0")):
         monkeypatch.setenv("RTMI_BLOCK_FLUSH", flush)
-        monkeypatch.setenv("RTMI_BLOCK_POOL", pool)
         monkeypatch.setenv("RTMI_BLOCK_OWNS", owns)
         r = rt.Renderer(final_world, 0)
         try:
@@ -557,7 +554,7 @@ def test_block_flush_same_image(accel, W, H, S, final_world, monkeypatch):
         assert sch["items_per_tile"] == 4 and sch["persistent"] == 0, sch
         # 4 items per tile on 4-wave blocks: the block owns its tile (2)
         assert sch["block_flush"] == (0 if flush == "0" else (2 if owns == "1" else 1)), sch
-        assert sch["block_pool"] == int(flush == "1" and pool == "1"), sch
+        assert sch["ray_pool"] == 1, sch
         if S == 5:
             assert sch["chunk"] == 2  # 2, 2, 1, 0 samples
     assert all(np.array_equal(imgs[0], im) for im in imgs[1:])

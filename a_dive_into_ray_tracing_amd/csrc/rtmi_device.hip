@@ -308,7 +308,7 @@ __device__ __forceinline__ bool path_segment(const SceneView<float> &sc, const S
   const float4 sh1k = sc.sh1[kk], sh0k = sc.sh0[kk], geomk = sc.geom[kk];
   const int kind = miss ? -1 : int(sh1k.x);
   float inv_len = 0.0f;
-  if (kind != RT_MAT_LAMBERTIAN) inv_len = 1.0f / dsqrt(dot<true>(d, d));
+  if (kind != RT_MAT_LAMBERTIAN) inv_len = drcp(dsqrt(dot<true>(d, d)));
   if (miss) {
     const V3<float> sk = sky_fast(d, inv_len);
     col = mk(T.x * sk.x, T.y * sk.y, T.z * sk.z);
@@ -2135,6 +2135,52 @@ RTMI_EXPORT int rt_ctx_debug_hits(rt_ctx *ctx, const float *rays, int32_t n, int
   (void)hipFree(d_rays);
   (void)hipFree(d_idx);
   (void)hipFree(d_t);
+  return RT_OK;
+}
+
+// Exhaustive check of the fast correctly rounded float routines (rtmi_path.h
+// sqrt_cr / rcp_cr) against the compiler's IEEE lowering: every one of the
+// 2^32 bit patterns (NaN == NaN whatever the payload).  out[0] mismatches,
+// out[1] the smallest mismatching input, out[2] / out[3] the two results
+// there.  Diagnostic (tests), not part of the render path.
+__global__ void exact_math_kernel(int32_t which, unsigned long long *res) {
+  const uint32_t base = (uint32_t(blockIdx.x) * blockDim.x + threadIdx.x) << 8;
+  unsigned bad = 0;
+  uint32_t first = 0xFFFFFFFFu, got_first = 0, want_first = 0;
+  for (uint32_t k = 0; k < 256; ++k) {
+    const uint32_t bits = base + k;
+    const float x = __uint_as_float(bits);
+    const float got = which == 0 ? sqrt_cr(x) : rcp_cr(x);
+    const float want = which == 0 ? __builtin_sqrtf(x) : 1.0f / x;
+    const bool same = __float_as_uint(got) == __float_as_uint(want) || (got != got && want != want);
+    if (!same) {
+      ++bad;
+      if (bits < first) { first = bits; got_first = __float_as_uint(got); want_first = __float_as_uint(want); }
+    }
+  }
+  if (bad) {
+    atomicAdd(&res[0], (unsigned long long)bad);
+    const unsigned long long old = atomicMin(&res[1], (unsigned long long)first);
+    if (first < old) { res[2] = got_first; res[3] = want_first; }  // (racy only between mismatching threads)
+  }
+}
+
+RTMI_EXPORT int rt_debug_exact_math(int32_t which, uint64_t *out) {
+  if (!out || which < 0 || which > 1) return set_error(RT_EINVAL, "rt_debug_exact_math: bad argument");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return set_error(RT_ENODEVICE, "no GPU");
+  unsigned long long *d = nullptr;
+  int rc;
+  if ((rc = dev_alloc(&d, 4))) return rc;
+  const unsigned long long init[4] = {0, ~0ull, 0, 0};
+  HIP_TRY(hipMemcpy(d, init, sizeof init, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(exact_math_kernel, dim3(1u << 16), dim3(256), 0, nullptr, which, d);  // 2^24 threads x 256
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipDeviceSynchronize());
+  unsigned long long v[4];
+  HIP_TRY(hipMemcpy(v, d, sizeof v, hipMemcpyDeviceToHost));
+  (void)hipFree(d);
+  for (int i = 0; i < 4; i++) out[i] = v[i];
   return RT_OK;
 }
 

@@ -36,8 +36,46 @@ template <bool F> __device__ __forceinline__ double madd(double a, double b, dou
   if constexpr (F) return __builtin_fma(a, b, c);
   else return a * b + c;
 }
+// Correctly rounded float sqrt and reciprocal in fewer instructions than the
+// compiler's IEEE lowering (~16 and ~10 VALU: denormal scaling, class checks,
+// v_div_scale / v_div_fmas / v_div_fixup), bit-identical to it for EVERY one
+// of the 2^32 inputs (rt_debug_exact_math checks all of them on the GPU:
+// tests/test_gpu_parity.py::test_exact_math_exhaustive).
+//  sqrt: the hardware v_sqrt_f32 (within 1 ulp), then the neighbour below or
+//  above when the exact residual x - s'*s says the true root lies past the
+//  midpoint (+inf passes through: its residuals are NaN); inputs below 2^-96
+//  keep the IEEE lowering.
+//  reciprocal: v_rcp_f32, then one Newton step with exact fma residual; the
+//  ranges where 1/x or x lies outside the normal range keep the IEEE
+//  division (a branch no realistic scene takes).
+#ifndef RTMI_EXACT_MATH
+#define RTMI_EXACT_MATH 1
+#endif
+__device__ __forceinline__ float sqrt_cr(float x) {
+  // below 2^-96 (zero, denormals — which v_sqrt_f32 flushes — negatives,
+  // NaN) the residuals would underflow: the IEEE lowering
+  if (!(x >= 0x1p-96f)) return __builtin_sqrtf(x);
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sm = __int_as_float(__float_as_int(s) - 1), sp = __int_as_float(__float_as_int(s) + 1);
+  float r = __builtin_fmaf(-sm, s, x) <= 0.0f ? sm : s;
+  r = __builtin_fmaf(-sp, s, x) > 0.0f ? sp : r;
+  return r;
+}
+__device__ __forceinline__ float rcp_cr(float x) {
+  const float ax = __builtin_fabsf(x);
+  if (!(ax >= 0x1p-125f && ax <= 0x1p+125f)) return 1.0f / x;  // zero, denormal, huge, inf, NaN
+  const float r = __builtin_amdgcn_rcpf(x);
+  return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+}
+#if RTMI_EXACT_MATH
+__device__ __forceinline__ float dsqrt(float x) { return sqrt_cr(x); }
+__device__ __forceinline__ float drcp(float x) { return rcp_cr(x); }
+#else
 __device__ __forceinline__ float dsqrt(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ float drcp(float x) { return 1.0f / x; }
+#endif
 __device__ __forceinline__ double dsqrt(double x) { return __builtin_sqrt(x); }
+__device__ __forceinline__ double drcp(double x) { return 1.0 / x; }
 __device__ __forceinline__ float dfabs(float x) { return __builtin_fabsf(x); }
 __device__ __forceinline__ double dfabs(double x) { return __builtin_fabs(x); }
 __device__ __forceinline__ float dfmin(float a, float b) { return __builtin_fminf(a, b); }
@@ -54,7 +92,7 @@ template <bool F, class R> __device__ __forceinline__ R dot(V3<R> a, V3<R> b) {
 template <class R> __device__ __forceinline__ V3<R> scale(R t, V3<R> v) { return mk(t * v.x, t * v.y, t * v.z); }
 // unit_vector vec3.h:101 (operator/ is (1/t)*v, vec3.h:89)
 template <bool F, class R> __device__ __forceinline__ V3<R> unit(V3<R> v) {
-  return scale(R(1) / dsqrt(dot<F>(v, v)), v);
+  return scale(drcp(dsqrt(dot<F>(v, v))), v);
 }
 // reflect vec3.h:114
 template <bool F, class R> __device__ __forceinline__ V3<R> reflect(V3<R> v, V3<R> n) {
@@ -146,7 +184,7 @@ __device__ __forceinline__ V3<float> unit_dir(Xoro &g) {
   float u, v, c, s;
   g.pair(u, v);
   const float z = __builtin_fmaf(-2.0f, u, 1.0f);
-  const float r = __builtin_sqrtf(__builtin_fmaf(-z, z, 1.0f));
+  const float r = dsqrt(__builtin_fmaf(-z, z, 1.0f));
   sincos2pi(v, c, s);
   return mk(r * c, r * s, z);
 }
@@ -161,7 +199,7 @@ __device__ __forceinline__ V3<float> in_sphere_direct(Xoro &g) {
 __device__ __forceinline__ V3<float> in_disk_direct(Xoro &g) {
   float u, v, c, s;
   g.pair(u, v);
-  const float r = __builtin_sqrtf(u);
+  const float r = dsqrt(u);
   sincos2pi(v, c, s);
   return mk(r * c, r * s, 0.0f);
 }
@@ -246,7 +284,7 @@ __device__ __forceinline__ void get_ray(const Cam<R> &c, R s, R t, G &g, V3<R> &
 template <bool F, class R>
 __device__ __forceinline__ int32_t hit_world(const SceneView<R> &sc, V3<R> o, V3<R> d, R &t_hit) {
   const R a = dot<F>(d, d);
-  const R inv_a = R(1) / a;
+  const R inv_a = drcp(a);
   const R t_min = R(0.001);
   R t_max = R(INFINITY);
   int32_t best = -1;
@@ -299,7 +337,7 @@ __device__ __forceinline__ int32_t hit_world_packed(const SpherePair *__restrict
 #endif
                                                     ) {
   const float a = dot<true>(d, d);
-  const float inv_a = 1.0f / a;
+  const float inv_a = drcp(a);
   const float K = dot<true>(o, d);
   const float aL = a * dot<true>(o, o);
   const float n2a = -2.0f * a;
@@ -521,7 +559,7 @@ struct PhaseClock { unsigned long long c[3]; };
 // they can be promoted to registers).
 #define RTMI_RAY_TERMS(o, d)                                    \
   const float a = dot<true>(d, d);                              \
-  const float inv_a = 1.0f / a;                                 \
+  const float inv_a = drcp(a);                                  \
   const float K = dot<true>(o, d);                              \
   const float aL = a * dot<true>(o, o);                         \
   const float n2a = -2.0f * a;                                  \
@@ -894,7 +932,7 @@ __device__ __forceinline__ bool scatter_fast(const float4 s0, const float4 s1, V
   }
   if (kind != RT_MAT_DIELECTRIC) {  // lambertian, metal: unit_dir from (u, v)
     const float z = __builtin_fmaf(-2.0f, u, 1.0f);
-    const float r = __builtin_sqrtf(__builtin_fmaf(-z, z, 1.0f));
+    const float r = dsqrt(__builtin_fmaf(-z, z, 1.0f));
     float c, sn;
     sincos2pi(v, c, sn);
     const V3<float> ru = mk(r * c, r * sn, z);
@@ -963,7 +1001,7 @@ __device__ __forceinline__ V3<float> sky_fast(V3<float> d, float inv_len) {
   return mk(__builtin_fmaf(t, 0.5f, 1.0f - t), __builtin_fmaf(t, 0.7f, 1.0f - t), __builtin_fmaf(t, 1.0f, 1.0f - t));
 }
 template <bool F, class R> __device__ __forceinline__ V3<R> sky(V3<R> d) {
-  const R uy = (R(1) / dsqrt(dot<F>(d, d))) * d.y;
+  const R uy = drcp(dsqrt(dot<F>(d, d))) * d.y;
   const R t = R(0.5) * (uy + R(1));
   return mk(madd<F>(t, R(0.5), R(1) - t), madd<F>(t, R(0.7), R(1) - t), madd<F>(t, R(1), R(1) - t));
 }

@@ -730,3 +730,18 @@ def test_config3_strips_unpermute_to_config2_frame(G, config2, final_world):
         r.close()
     assert all(not s[-1].any() for s in strips[H % G or G:]), "rows past H must be zero-filled"
     assert np.array_equal(rdist.unpermute(strips, H), img)
+
+
+@pytest.mark.parametrize("which", [0, 1], ids=["sqrt", "reciprocal"])
+def test_exact_math_exhaustive(which):
+    """The kernels' short correctly rounded sqrt and reciprocal (rtmi_path.h
+    sqrt_cr / rcp_cr: v_sqrt_f32 / v_rcp_f32 plus an exact-residual
+    correction) equal the compiler's IEEE lowering — and so glibc's sqrtf
+    and the division the oracle computes — for every one of the 2^32 float
+    bit patterns (zeros, denormals, infinities and NaNs included)."""
+    f = rt.load().rt_debug_exact_math
+    f.argtypes = [C.c_int32, C.POINTER(C.c_uint64)]
+    f.restype = C.c_int
+    v = (C.c_uint64 * 4)()
+    rt.check(f(which, v), "rt_debug_exact_math")
+    assert v[0] == 0, f"{v[0]} mismatches; first input {v[1]:#010x}: got {v[2]:#010x}, IEEE {v[3]:#010x}"

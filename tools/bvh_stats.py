@@ -1,4 +1,5 @@
-"""BVH traversal statistics of the RTMI_STATS build at config 2 (GPU box)."""
+"""BVH / grid walk statistics of the RTMI_STATS build at config 2 (GPU box).
+    python tools/bvh_stats.py [bvh|grid]"""
 import ctypes as C
 import os
 import sys
@@ -11,8 +12,9 @@ import a_dive_into_ray_tracing_amd as rt  # noqa: E402
 L = rt.load()
 L.rt_ctx_debug_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
 r = rt.Renderer(rt.random_scene(), 0)
-r.set_accel("bvh")
-print("accel info (big, nodes):", r.accel_info())
+accel = sys.argv[1] if len(sys.argv) > 1 else "bvh"
+r.set_accel(accel)
+print(accel, "accel info:", r.accel_info() if accel == "bvh" else r.grid_info())
 r.render(rt.final_camera(1.5), 1200, 800, 500, 50, 1984)
 v = (C.c_uint64 * 8)()
 L.rt_ctx_debug_counters(r._h, v)

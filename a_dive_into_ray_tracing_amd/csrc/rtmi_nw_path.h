@@ -77,7 +77,7 @@ __device__ __forceinline__ float nw_atanf(float x) {
   float a = neg ? -x : x, y0 = 0.0f;
   if (a > 2.414213562373095f) {
     y0 = 1.57079637f;
-    a = -1.0f / a;
+    a = -drcp(a);
   } else if (a > 0.4142135623730950f) {
     y0 = 0.785398185f;
     a = (a - 1.0f) / (a + 1.0f);
@@ -97,7 +97,7 @@ __device__ __forceinline__ float nw_atan2f(float y, float x) {
 }
 __device__ __forceinline__ float nw_acosf(float x) {
   x = __builtin_fminf(__builtin_fmaxf(x, -1.0f), 1.0f);
-  return nw_atan2f(__builtin_sqrtf((1.0f - x) * (1.0f + x)), x);
+  return nw_atan2f(dsqrt((1.0f - x) * (1.0f + x)), x);
 }
 
 // ---------------------------------------------------------------------------
@@ -166,7 +166,7 @@ __device__ __forceinline__ bool hit_sphere(V o, V d, V c, float r, float tmin, f
   const float cc = dot3(oc, oc) - r * r;
   const float disc = __builtin_fmaf(b, b, -(a * cc));
   if (disc > 0.0f) {
-    const float sq = __builtin_sqrtf(disc);
+    const float sq = dsqrt(disc);
     float tt = (-b - sq) / a;
     if (tt < tmax && tt > tmin) { t = tt; return true; }
     tt = (-b + sq) / a;
@@ -192,7 +192,7 @@ __device__ __forceinline__ bool hit_moving(V o, V d, V c, float r, float tmin, f
   const float cc = dot3(oc, oc) - r * r;
   const float disc = __builtin_fmaf(hb, hb, -(a * cc));
   if (disc < 0.0f) return false;
-  const float sq = __builtin_sqrtf(disc);
+  const float sq = dsqrt(disc);
   float root = (-hb - sq) / a;
   if (root < tmin || tmax < root) {
     root = (-hb + sq) / a;
@@ -314,7 +314,7 @@ __device__ __forceinline__ bool hit_medium(const Obj &ob, int32_t id, V o, V d, 
     const float a = dot3(d, d), b = dot3(oc, d), cc = dot3(oc, oc) - r * r;
     const float disc = __builtin_fmaf(b, b, -(a * cc));
     if (mv ? disc < 0.0f : !(disc > 0.0f)) return false;  // hit_moving / hit_sphere
-    const float sq = __builtin_sqrtf(disc);
+    const float sq = dsqrt(disc);
     const float q1 = (-b - sq) / a, q2 = (-b + sq) / a;
     auto pick = [&](float tmin, float tmax, float &out) {
       if (mv) {  // closed interval, hit_moving
@@ -333,7 +333,7 @@ __device__ __forceinline__ bool hit_medium(const Obj &ob, int32_t id, V o, V d, 
     if (!hit_boundary(ob, o, d, time, float(double(r1) + 0.00001), INFINITY, r2)) return false;
   }
   if (r1 < 0.0f) r1 = 0.0f;
-  const float len = __builtin_sqrtf(dot3(dw, dw));
+  const float len = dsqrt(dot3(dw, dw));
   const float inside = (r2 - r1) * len;
   const int samples = ob.aux >> 8;
   bool hit = false;
@@ -392,11 +392,11 @@ __device__ __forceinline__ bool hit_object(const View &sc, const DevObj &ob, V o
     case kSphere: return hit_sphere(o, d, mk(ob.g0[0], ob.g0[1], ob.g0[2]), ob.g0[3], tmin, INFINITY, t);
     case kMovingSphere: return hit_moving(o, d, moving_center(ob, time), ob.g0[3], tmin, INFINITY, t);
     case kRectXY: case kRectXZ: case kRectYZ: {
-      const V inv = local ? mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z) : invw;
+      const V inv = local ? mk(drcp(d.x), drcp(d.y), drcp(d.z)) : invw;
       return hit_rect_kind_inv(kind, o, d, inv, ld4(ob.g0), ob.g1[0], tmin, INFINITY, t);
     }
     default: {
-      const V inv = local ? mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z) : invw;
+      const V inv = local ? mk(drcp(d.x), drcp(d.y), drcp(d.z)) : invw;
       face = hit_box_inv(o, d, inv, ld4(ob.g0), ld4(ob.g1), tmin, INFINITY, t);
       return face >= 0;
     }
@@ -427,7 +427,7 @@ __device__ __forceinline__ int32_t hit_world_nw(const View &sc, V o, V d, float 
   int32_t best = -1, best_id = 0x7fffffff;
   best_face = -1;
   uint32_t med_hit = 0;
-  const V invw = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // hit_object's planes
+  const V invw = mk(drcp(d.x), drcp(d.y), drcp(d.z));  // hit_object's planes
   for (int32_t m = 0; m < sc.nmed; ++m) {
     const Obj ob = sc.med[m];
     const int32_t id = sc.med_id[m];
@@ -444,7 +444,7 @@ __device__ __forceinline__ int32_t hit_world_nw(const View &sc, V o, V d, float 
       }
     }
   }
-  auto safe_inv = [](float v) { return 1.0f / (__builtin_fabsf(v) < 1e-20f ? __builtin_copysignf(1e-20f, v) : v); };
+  auto safe_inv = [](float v) { return drcp(__builtin_fabsf(v) < 1e-20f ? __builtin_copysignf(1e-20f, v) : v); };
   const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
   const float ox = -o.x * ix, oy = -o.y * iy, oz = -o.z * iz;
   int32_t node = 0;
@@ -524,7 +524,7 @@ __device__ __forceinline__ int32_t hit_world_nw_grid(const View &sc, V o, V d, f
   uint32_t med_hit = 0;
   V invw = mk(0.f, 0.f, 0.f);
   if constexpr (!S) {
-    invw = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // hit_object's planes
+    invw = mk(drcp(d.x), drcp(d.y), drcp(d.z));  // hit_object's planes
     for (int32_t m = 0; m < sc.nmed; ++m) {
       const Obj ob = sc.med[m];
       const int32_t id = sc.med_id[m];
@@ -732,7 +732,7 @@ __device__ __forceinline__ Rec make_rec(const View &sc, const DevObj &ob, V ow, 
   r.v = 0.0f;
   if constexpr (S) {  // a sphere, no instance, no texture reads u, v
     const V c = (ob.ka & 255) == kSphere ? mk(ob.g0[0], ob.g0[1], ob.g0[2]) : moving_center(ob, time);
-    const float inv_r = 1.0f / ob.g0[3];
+    const float inv_r = drcp(ob.g0[3]);
     const V p = at3(ow, dw, t);
     r.n = mk(inv_r * (p.x - c.x), inv_r * (p.y - c.y), inv_r * (p.z - c.z));
     r.p = p;
@@ -750,7 +750,7 @@ __device__ __forceinline__ Rec make_rec(const View &sc, const DevObj &ob, V ow, 
   const int okind = ob.ka & 255;
   if (okind == kSphere || okind == kMovingSphere) {
     const V c = okind == kSphere ? mk(ob.g0[0], ob.g0[1], ob.g0[2]) : moving_center(ob, time);
-    const float inv_r = 1.0f / ob.g0[3];
+    const float inv_r = drcp(ob.g0[3]);
     n = mk(inv_r * (p.x - c.x), inv_r * (p.y - c.y), inv_r * (p.z - c.z));
     if (need_uv) sphere_uv(n, r.u, r.v);
   } else {
@@ -818,17 +818,17 @@ __device__ __forceinline__ bool scatter_nw(const View &sc, const Rec &rec, V din
       const V reflected = reflect<true>(din, n);
       atten = mk(1.0f, 1.0f, 1.0f);
       const float dn = dot3(din, n);
-      const float dlen = __builtin_sqrtf(dot3(din, din));
+      const float dlen = dsqrt(dot3(din, din));
       V outward;
       float ni, cosine;
       if (dn > 0.0f) {
         outward = mk(-n.x, -n.y, -n.z);
         ni = m.ir;
         cosine = dn / dlen;
-        cosine = __builtin_sqrtf(1.0f - (m.ir * m.ir) * __builtin_fmaf(-cosine, cosine, 1.0f));
+        cosine = dsqrt(1.0f - (m.ir * m.ir) * __builtin_fmaf(-cosine, cosine, 1.0f));
       } else {
         outward = n;
-        ni = 1.0f / m.ir;
+        ni = drcp(m.ir);
         cosine = -dn / dlen;
       }
       const V uv = unit<true>(din);
@@ -837,7 +837,7 @@ __device__ __forceinline__ bool scatter_nw(const View &sc, const Rec &rec, V din
       V refracted = mk(0.f, 0.f, 0.f);
       float reflect_prob = 1.0f;
       if (disc > 0.0f) {
-        const float sq = __builtin_sqrtf(disc);
+        const float sq = dsqrt(disc);
         refracted = mk(__builtin_fmaf(-outward.x, sq, ni * __builtin_fmaf(-outward.x, dt, uv.x)),
                        __builtin_fmaf(-outward.y, sq, ni * __builtin_fmaf(-outward.y, dt, uv.y)),
                        __builtin_fmaf(-outward.z, sq, ni * __builtin_fmaf(-outward.z, dt, uv.z)));

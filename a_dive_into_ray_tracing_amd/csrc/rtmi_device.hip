@@ -98,7 +98,7 @@ __device__ unsigned g_trace_n;
 #define RTMI_TRACE_BEGIN                                                                 \
   const unsigned long long trace_t0 = __builtin_amdgcn_s_memrealtime();                  \
   const unsigned long long cyc_start = __builtin_amdgcn_s_memtime();
-#define RTMI_TRACE_END(items)                                                            \
+#define RTMI_TRACE_END(items, wsegs)                                                     \
   if (lane == 0) {                                                                       \
     atomicAdd(&segments[5], cnt.cyc_hit);                                                \
     atomicAdd(&segments[6], __builtin_amdgcn_s_memtime() - cyc_start);                   \
@@ -109,12 +109,12 @@ __device__ unsigned g_trace_n;
       g_trace[4 * k_ + 2] = (uint64_t(__builtin_amdgcn_s_getreg(0xF804)) << 32) |        \
                             uint64_t(unsigned(items));                                   \
       g_trace[4 * k_ + 3] = (uint64_t(blockIdx.x * (blockDim.x >> 6) + wave) << 32) |     \
-                            (wave_segs[wave] & 0xFFFFFFFFull);                           \
+                            (uint64_t(wsegs) & 0xFFFFFFFFull);                           \
     }                                                                                    \
   }
 #else
 #define RTMI_TRACE_BEGIN
-#define RTMI_TRACE_END(items)
+#define RTMI_TRACE_END(items, wsegs)
 #endif
 
 // RTMI_CHECK builds (analysis only) bounds-check every accumulator write and
@@ -137,7 +137,7 @@ constexpr int kRayPool = RTMI_RAY_POOL;
 constexpr int kPairGroup = RTMI_PAIR_GROUP;  // sphere pairs per scalar-load group
 
 // Per-sample colour -> int64 fixed point (2^-32).  Guarded: NaN -> 0 and
-// the value clamped to [-64, 64], so the conversion is always defined and a
+// the value clamped to [0, 64], so the conversion is always defined and a
 // sum of up to 2^24 samples cannot overflow (64 * 2^24 * 2^32 = 2^62);
 // every scene here stays far inside (RTIOW colours are <= 1).  The oracle
 // applies the identical guard.
@@ -151,9 +151,14 @@ __device__ __forceinline__ int div_small(int q, int d, float inv_d) {
 }
 
 __device__ __forceinline__ int64_t to_fixed(float c) {
-  // branch-free: v_med3 clamps (inf included), NaN selects 0
-  const float g = c == c ? __builtin_amdgcn_fmed3f(c, -64.0f, 64.0f) : 0.0f;
-  return int64_t(g * 4294967296.0f);
+  // branch-free: v_med3 clamps to [0, 64] (inf included), NaN selects 0; then
+  // trunc(g * 2^32) as two 32-bit halves (g >= 0: trunc = floor): the
+  // integer part, and the fraction (exact) scaled by 2^32 (exact, < 2^32) —
+  // 8 VALU instead of the 64-bit conversion's 15
+  const float g = c == c ? __builtin_amdgcn_fmed3f(c, 0.0f, 64.0f) : 0.0f;
+  const uint32_t hi = uint32_t(g);
+  const uint32_t lo = uint32_t((g - float(hi)) * 4294967296.0f);
+  return int64_t((uint64_t(hi) << 32) | lo);
 }
 __device__ __forceinline__ float from_fixed(int64_t v) { return float(v) * 0x1p-32f; }
 
@@ -345,7 +350,6 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   constexpr int TH = 64 / TW;
   constexpr int WPB = GridShape<ACC != 0>::waves;
   __shared__ unsigned long long acc[WPB][3][64];
-  __shared__ unsigned long long wave_segs[WPB];
   __shared__ float cam_lds[21];  // the camera (stage_camera)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -377,8 +381,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   acc[wave][0][lane] = 0;
   acc[wave][1][lane] = 0;
   acc[wave][2][lane] = 0;
-  if (lane == 0) wave_segs[wave] = 0;
-  unsigned nseg = 0;  // world.hit calls of this lane (algorithmic-work accounting)
+  unsigned nseg = 0;  // world.hit calls of this wave (wave-uniform; algorithmic-work accounting)
   RTMI_TRACE_BEGIN
   SegCounters cnt{};
 #if RTMI_TRACE_PHASES
@@ -457,14 +460,15 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
 #endif
 
   for (;;) {
-    if (__ballot(active) == 0) break;
+    const unsigned long long live = __ballot(active);
+    if (live == 0) break;
+    nseg += unsigned(__popcll(live));
     bool done = false;
     V3<float> col = mk(0.f, 0.f, 0.f);
 #if RTMI_TRACE_PHASES
     const unsigned long long cyc_a = __builtin_amdgcn_s_memtime();
 #endif
     if (active) {
-      ++nseg;
       done = path_segment<ACC>(sc, pairs, a, o, d, T, depth, rng, col, cnt, segments);
     }
 #if RTMI_TRACE_PHASES
@@ -526,12 +530,9 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
 #endif
   }
 
-  atomicAdd(&wave_segs[wave], (unsigned long long)nseg);
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
   if (lane == 0) {
-    atomicAdd(segments, wave_segs[wave]);
-    if (a.tile_cost) atomicAdd(&a.tile_cost[tile], unsigned(wave_segs[wave]));
+    atomicAdd(segments, (unsigned long long)nseg);
+    if (a.tile_cost) atomicAdd(&a.tile_cost[tile], nseg);
   }
   flush_counters(cnt, lane, segments);
 #if RTMI_TRACE_PHASES
@@ -543,7 +544,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   // wave-level: [4] hit + shading passes, [7] accumulation + regeneration
   if (lane == 0) { atomicAdd(&segments[4], cyc_iter); atomicAdd(&segments[7], cyc_regen); }
 #endif
-  RTMI_TRACE_END(1)
+  RTMI_TRACE_END(1, nseg)
   if constexpr (CHUNKED) {
     if (a.block_flush) {  // block-uniform; no wave of this block returned early
       __syncthreads();
@@ -808,7 +809,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
   __builtin_amdgcn_wave_barrier();
   if (lane == 0) atomicAdd(segments, wave_segs[wave]);
   flush_counters(cnt, lane, segments);
-  RTMI_TRACE_END(n_taken)
+  RTMI_TRACE_END(n_taken, wave_segs[wave])
   (void)n_taken;
 }
 

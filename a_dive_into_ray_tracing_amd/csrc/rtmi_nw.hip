@@ -109,10 +109,12 @@ __device__ unsigned long long g_nw_phase[4];
 __device__ unsigned long long g_nw_stats[4];
 #endif
 
-// NaN -> 0, clamped to [-64, 64]: as rtmi_device.hip to_fixed (and the oracle)
+// NaN -> 0, clamped to [0, 64]: as rtmi_device.hip to_fixed (and the oracle)
 __device__ __forceinline__ int64_t fixed(float c) {
-  const float g = c == c ? __builtin_amdgcn_fmed3f(c, -64.0f, 64.0f) : 0.0f;  // branch-free guard
-  return int64_t(g * 4294967296.0f);
+  const float g = c == c ? __builtin_amdgcn_fmed3f(c, 0.0f, 64.0f) : 0.0f;  // branch-free guard
+  const uint32_t hi = uint32_t(g);
+  const uint32_t lo = uint32_t((g - float(hi)) * 4294967296.0f);
+  return int64_t((uint64_t(hi) << 32) | lo);
 }
 
 // The camera, shutter and image size in LDS (23 floats), read at each

@@ -190,9 +190,9 @@ __device__ __forceinline__ V3<float> unit_dir(Xoro &g) {
 }
 __device__ __forceinline__ V3<float> in_sphere_direct(Xoro &g) {
   const V3<float> d = unit_dir(g);
-  float a, b, c, unused;
+  float a, b;
   g.pair(a, b);
-  g.pair(c, unused);
+  const float c = g.uni();  // = the first of a pair, one step
   const float r = __builtin_fmaxf(a, __builtin_fmaxf(b, c));
   return mk(r * d.x, r * d.y, r * d.z);
 }
@@ -944,9 +944,9 @@ __device__ __forceinline__ bool scatter_fast(const float4 s0, const float4 s1, V
       return true;
     }
     // metal material.h:40-49: a point in the ball = ru * max of three uniforms
-    float a, b, cc, unused;
+    float a, b;
     g.pair(a, b);
-    g.pair(cc, unused);
+    const float cc = g.uni();  // = the first of a pair, one step
     const float rr = __builtin_fmaxf(a, __builtin_fmaxf(b, cc));
     const V3<float> rv = mk(rr * ru.x, rr * ru.y, rr * ru.z);
     const float fz = s1.y;

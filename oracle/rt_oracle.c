@@ -392,9 +392,11 @@ int32_t or_ref_scatter(int32_t kind, const double mat[4], const double din[3], c
 /* ---------------------------------------------------------------------- */
 /* per-sample colour -> int64 fixed point, 2^-32 units (truncation) */
 /* the kernel's guarded conversion (rtmi_device.hip to_fixed): NaN -> 0,
- * clamped to [-64, 64] so the cast is defined and 2^24-sample sums fit */
+ * clamped to [0, 64] so the cast is defined and 2^24-sample sums fit (a
+ * sample's colour is a product of albedos and sky or emission: non-negative
+ * in every scene the reference builds) */
 static inline int64_t to_fixed(float c) {
-  const float g = c == c ? (c > 64.0f ? 64.0f : (c < -64.0f ? -64.0f : c)) : 0.0f;
+  const float g = c == c ? (c > 64.0f ? 64.0f : (c < 0.0f ? 0.0f : c)) : 0.0f;
   return (int64_t)(g * 4294967296.0f);
 }
 static inline float from_fixed(int64_t v) { return (float)v * 0x1p-32f; }

@@ -117,8 +117,9 @@ def test_direct_point_in_disk():
 
 def test_fixed_point_guard_non_finite_colours():
     """The oracle's fixed-point conversion (mirrored by the kernels' to_fixed):
-    NaN -> 0, values clamped to [-64, 64], so sums stay finite.  A NaN albedo
-    and an overflowing one (1e30: attenuation -> inf) produce such colours."""
+    NaN -> 0, values clamped to [0, 64], so sums stay finite (and a negative
+    albedo cannot make a negative sum).  A NaN albedo, an overflowing one
+    (1e30: attenuation -> inf) and a negative one produce such colours."""
     import ctypes as C
 
     import a_dive_into_ray_tracing_amd as rt
@@ -126,9 +127,11 @@ def test_fixed_point_guard_non_finite_colours():
     world = rt.learn_scene()
     world.mat_params[1, :3] = [np.nan, 0.5, 0.5]
     world.mat_params[4, :3] = [1e30, 1e30, 1e30]
+    world.mat_params[0, :3] = [-0.5, 0.5, 0.5]  # ground: negative red
     cam = rt.learn_camera(40 / 24)
     c = O.OrCamera()
     C.memmove(C.byref(c), C.byref(cam), C.sizeof(c))
     out = O.fast_render(O.Scene(world.center_radius, world.mat_kind, world.mat_params), c, 40, 24, 8, 50, 1984)
     assert np.isfinite(out).all()
     assert out.max() == 64.0 * 8  # a pixel whose 8 samples all saturate
+    assert out.min() >= 0.0

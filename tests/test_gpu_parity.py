@@ -609,11 +609,12 @@ def test_cost_probe_same_image_and_count(accel, final_world, final_renderer):
 
 def test_non_finite_sample_colours_are_guarded():
     """A NaN albedo (and an overflowing one) make non-finite path colours; the
-    fixed-point conversion maps NaN to 0 and clamps to [-64, 64] on the GPU
+    fixed-point conversion maps NaN to 0 and clamps to [0, 64] on the GPU
     exactly as in the oracle, so the sums stay finite and bit-exact."""
     world = rt.learn_scene()
     world.mat_params[1, :3] = [np.nan, 0.5, 0.5]  # centre sphere: NaN red channel
     world.mat_params[4, :3] = [1e30, 1e30, 1e30]  # right (metal) sphere: attenuation overflows to inf
+    world.mat_params[0, :3] = [-0.5, 0.5, 0.5]  # ground: negative red (clamped to 0 per sample)
     W, H, S = 40, 24, 8
     cam = rt.learn_camera(W / H)
     r = rt.Renderer(world, 0)
@@ -625,6 +626,7 @@ def test_non_finite_sample_colours_are_guarded():
     assert np.isfinite(got).all()
     assert np.array_equal(got, want)
     assert got.max() == 64.0 * S or got.max() > 1.0 * S  # the clamp was reached somewhere
+    assert got.min() >= 0.0
 
 
 # ------------------------------------------------------------ config 5 -----

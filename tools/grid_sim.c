@@ -17,6 +17,12 @@
  *   ideal/K   all of the tile's segments sorted by key K (an upper bound on any regrouping)
  * keys: oct = direction octant; cell = entry cell; oct+cell; len = the walk's own cell count (oracle)
  *
+ * Also (round 3): the walk split by primary (camera) and secondary segments;
+ * per sphere iteration whether any lane has a candidate (disc >= 0) and
+ * whether any lane accepts a root (what a sqrt-free reject filter could skip
+ * at wave level); and a "flattened" schedule testing the round's (lane,
+ * sphere) pairs over all 64 lanes.
+ *
  *   gcc -O2 -o /tmp/grid_sim tools/grid_sim.c -lm && /tmp/grid_sim tests/golden/scene_final.txt [spp] [stride]
  */
 #include <math.h>
@@ -36,8 +42,9 @@ static double rnd(void) {
   return (rs >> 11) * (1.0 / 9007199254740992.0);
 }
 
-typedef struct { double o[3], d[3]; } Ray;
-static Ray *segs; static int nseg, capseg;
+typedef struct { double o[3], d[3]; int depth; } Ray;
+static unsigned long long *g_cand, *g_use;
+static Ray *segs; static int nseg, capseg, cur_depth;
 static int *tile_start; static int ntiles, captiles;
 
 static int hit_bf(const double o[3], const double d[3], double *tt) {
@@ -63,7 +70,7 @@ static void rand_unit(double v[3]) {
 
 static void push(const double o[3], const double d[3]) {
   if (nseg == capseg) { capseg = capseg ? 2*capseg : 1<<20; segs = realloc(segs, capseg*sizeof(Ray)); }
-  memcpy(segs[nseg].o, o, 24); memcpy(segs[nseg].d, d, 24); nseg++;
+  memcpy(segs[nseg].o, o, 24); memcpy(segs[nseg].d, d, 24); segs[nseg].depth = cur_depth; nseg++;
 }
 
 /* ---- grid (build_grid's shape: small spheres, margin-grown boxes, ~0.3 cells per sphere) ---- */
@@ -127,15 +134,17 @@ static int walk(const Ray *r, int *lens, int *entry_cell) {
   int nc = 0;
   for (;;) {
     int cell = c[0] + n[0]*(c[1] + n[1]*c[2]);
-    lens[nc++] = cell_start[cell+1] - cell_start[cell];
+    lens[nc] = cell_start[cell+1] - cell_start[cell]; g_cand[nc] = 0; g_use[nc] = 0; nc++;
     /* the spheres tested here can only shrink tmax */
     for (int i = cell_start[cell]; i < cell_start[cell+1]; i++) { int q = cell_refs[i];
       double oc[3] = {r->o[0]-C[q][0], r->o[1]-C[q][1], r->o[2]-C[q][2]};
       double hb = oc[0]*r->d[0]+oc[1]*r->d[1]+oc[2]*r->d[2];
       double cc = oc[0]*oc[0]+oc[1]*oc[1]+oc[2]*oc[2]-C[q][3]*C[q][3];
       double disc = hb*hb - a*cc; if (disc < 0) continue;
+      int pos = i - cell_start[cell]; if (pos < 64) g_cand[nc-1] |= 1ull << pos;
       double sq = sqrt(disc), rt = (-hb-sq)/a;
       if (rt < 0.001 || rt > tmax) { rt = (-hb+sq)/a; if (rt < 0.001 || rt > tmax) continue; }
+      if (pos < 64) g_use[nc-1] |= 1ull << pos;
       tmax = rt; }
     int k = tnext[0] <= tnext[1] && tnext[0] <= tnext[2] ? 0 : (tnext[1] <= tnext[2] ? 1 : 2);
     if (!(tnext[k] < tmax)) break;
@@ -146,7 +155,7 @@ static int walk(const Ray *r, int *lens, int *entry_cell) {
   return nc;
 }
 
-typedef struct { int nc, oct, cell, lens[128]; } Walk;
+typedef struct { int nc, oct, cell, lens[128]; unsigned long long cand[128], use[128]; } Walk;
 static Walk *W;
 static int key_mode;
 static int key_of(const Walk *w) {
@@ -265,7 +274,7 @@ int main(int argc, char **argv) {
       double o[3], d[3];
       for (int a = 0; a < 3; a++) { o[a] = org[a] + cu[a]*dx + cv[a]*dy; d[a] = llc[a] + u*hor[a] + v*ver[a] - o[a]; }
       for (int depth = 0; depth < 50; depth++) {
-        push(o, d);
+        cur_depth = depth; push(o, d);
         double t; int k = hit_bf(o, d, &t);
         if (k < 0) break;
         double pp[3], nn[3], r = C[k][3];
@@ -300,6 +309,7 @@ int main(int argc, char **argv) {
   build(getenv("DENSITY") ? atof(getenv("DENSITY")) : 0.3);
   W = malloc(nseg * sizeof(Walk));
   for (int i = 0; i < nseg; i++) {
+    g_cand = W[i].cand; g_use = W[i].use;
     W[i].nc = walk(&segs[i], W[i].lens, &W[i].cell);
     W[i].oct = (segs[i].d[0] < 0) | ((segs[i].d[1] < 0) << 1) | ((segs[i].d[2] < 0) << 2);
   }
@@ -307,6 +317,42 @@ int main(int argc, char **argv) {
   Acc a = {0};
   for (int i = 0; i < nseg; i += 64) { int nl = nseg - i < 64 ? nseg - i : 64; for (int l = 0; l < nl; l++) ids[l] = i + l; wave_cost(ids, nl, &a); }
   report("shuffled", &a);
+
+  { double flat = 0, mx = 0, rounds = 0;
+    for (int i = 0; i < nseg; i += 64) { int nl = nseg - i < 64 ? nseg - i : 64; int maxc = 0;
+      for (int l = 0; l < nl; l++) if (W[i+l].nc > maxc) maxc = W[i+l].nc;
+      for (int c = 0; c < maxc; c++) { int m = 0, sum = 0; for (int l = 0; l < nl; l++) if (c < W[i+l].nc) { sum += W[i+l].lens[c]; if (W[i+l].lens[c] > m) m = W[i+l].lens[c]; }
+        mx += m; flat += (sum + 63) / 64; rounds++; } }
+    printf("  flattened rounds: per wave-seg rounds %.3f, sphere iterations lockstep %.3f vs flattened %.3f\n", rounds*64/nseg, mx*64/nseg, flat*64/nseg);
+  }
+
+  { double it = 0, anyc = 0, anyu = 0, lc = 0, lu = 0;
+    for (int i = 0; i < nseg; i += 64) { int nl = nseg - i < 64 ? nseg - i : 64; int maxc = 0;
+      for (int l = 0; l < nl; l++) if (W[i+l].nc > maxc) maxc = W[i+l].nc;
+      for (int c = 0; c < maxc; c++) { int m = 0; for (int l = 0; l < nl; l++) if (c < W[i+l].nc && W[i+l].lens[c] > m) m = W[i+l].lens[c];
+        for (int k = 0; k < m; k++) { int ac = 0, au = 0; it++;
+          for (int l = 0; l < nl; l++) { const Walk *w = &W[i+l]; if (c < w->nc && k < w->lens[c]) {
+            if ((w->cand[c] >> k) & 1) { ac = 1; lc++; } if ((w->use[c] >> k) & 1) { au = 1; lu++; } } }
+          anyc += ac; anyu += au; } } }
+    printf("  sphere iterations per wave-seg %.3f: any lane candidate %.3f, any lane accepted %.3f; per lane-seg candidates %.3f accepted %.3f\n",
+      it*64/nseg, anyc*64/nseg, anyu*64/nseg, lc/nseg, lu/nseg);
+  }
+
+  { Acc p = {0}, q = {0}, r = {0}; int np = 0;
+    for (int i = 0; i < nseg; i += 64) { int nl = nseg - i < 64 ? nseg - i : 64; int ip[64], is[64], npp = 0, ns = 0;
+      for (int l = 0; l < nl; l++) { if (segs[i+l].depth == 0) ip[npp++] = i + l; else is[ns++] = i + l; }
+      np += npp;
+      if (npp) wave_cost(ip, npp, &p);
+      if (ns) wave_cost(is, ns, &q); }
+    printf("  primary share %.3f\n", (double)np / nseg);
+    report("primary-only", &p); report("second-only", &q);
+    /* per-lane averages by kind */
+    double pc=0, ps=0, sc=0, ss=0; int npr=0, nse=0;
+    for (int i = 0; i < nseg; i++) { double cs = 0; for (int k = 0; k < W[i].nc; k++) cs += W[i].lens[k];
+      if (segs[i].depth == 0) { pc += W[i].nc; ps += cs; npr++; } else { sc += W[i].nc; ss += cs; nse++; } }
+    printf("  per-lane: primary cells %.3f spheres %.3f | secondary cells %.3f spheres %.3f\n", pc/npr, ps/npr, sc/nse, ss/nse);
+    (void)r;
+  }
   for (int i = 0; i < nseg; i += 64) { int nl = nseg - i < 64 ? nseg - i : 64; for (int l = 0; l < nl; l++) ids[l] = i + l; unified_cost(ids, nl); }
   printf("  one loop (if-if): iterations %.3f per wave-segment: with a sphere test %.3f, with a cell step %.3f\n",
          u_nt * 64 / nseg, u_ns * 64 / nseg, u_nc * 64 / nseg);

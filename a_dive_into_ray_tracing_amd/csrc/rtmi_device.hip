@@ -150,6 +150,9 @@ __device__ __forceinline__ int div_small(int q, int d, float inv_d) {
   return t;
 }
 
+// a wave-uniform float pinned to a scalar register
+__device__ __forceinline__ float uniform_f(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+
 __device__ __forceinline__ int64_t to_fixed(float c) {
   // branch-free: v_med3 clamps to [0, 64] (inf included), NaN selects 0; then
   // trunc(g * 2^32) as two 32-bit halves (g >= 0: trunc = floor): the
@@ -336,7 +339,9 @@ __device__ __forceinline__ bool path_segment(const SceneView<float> &sc, const S
   if (dot<true>(nd, nrm) < 0.f) delta = -delta;
   o = mk(__builtin_fmaf(delta, nrm.x, p.x), __builtin_fmaf(delta, nrm.y, p.y), __builtin_fmaf(delta, nrm.z, p.z));
   d = nd;
-  return ++depth >= a.max_depth;  // depth exhausted: black, main.cpp:58-60
+  // depth exhausted: black, main.cpp:58-60 (the depth is the low 24 bits:
+  // render_kernel keeps the path's pixel above them)
+  return (++depth & 0xFFFFFF) >= a.max_depth;
 }
 
 // ACC: 0 brute force, 1 BVH, 2 uniform grid (RT_ACCEL_*), 3 the grid walked as one
@@ -391,20 +396,24 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   const SceneView<float> sc{geom, sh0, sh1, a.n};
 
   V3<float> o, d, T;
-  int px = 0, depth = 0;
+  // the path's pixel in the tile (bits 24..29) and its depth (bits 0..23;
+  // max_depth < 2^24, check_render_args) in one register
+  int pxd = 0;
   bool active = true;
   Xoro rng;
 
   // job q -> pixel px = q % nv, sample s0 + q / nv (sample-major, so every
   // pixel of the tile advances together); then the camera ray.
-  // q / nv and px / vw by a float reciprocal with one correction step:
-  // exact for q < 2^22 (a job index here is < 64 * spp per item)
-  const float inv_nv = 1.0f / float(max(nv, 1)), inv_vw = 1.0f / float(vw);
+  // q / d = umulhi(2q, ceil(2^31 / d)), exact for 1 <= d <= 64 and q < 2^25
+  // (the error q (m d - 2^31) / (d 2^31) < q / 2^31 stays below 1/d; job
+  // indices are < 2^22); the multipliers are wave-uniform integers (scalar
+  // registers)
+  const uint32_t m_nv = 0x7FFFFFFFu / uint32_t(max(nv, 1)) + 1u, m_vw = 0x7FFFFFFFu / uint32_t(vw) + 1u;
   auto camera_ray = [&](int q, V3<float> &ro, V3<float> &rd, Xoro &g) {
-    const int qs = div_small(q, nv, inv_nv);
+    const int qs = int(__umulhi(uint32_t(q) << 1, m_nv));
     const int s = s0 + qs;
     const int p = q - qs * nv;
-    const int ly = div_small(p, vw, inv_vw), lx = p - ly * vw;
+    const int ly = int(__umulhi(uint32_t(p) << 1, m_vw)), lx = p - ly * vw;
     const int i = x0 + lx;
     const int j = a.row0 + (y0 + ly) * a.row_step;
     g.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(a.s_base + s));
@@ -422,9 +431,8 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
       o = ro;
       d = rd;
       rng = g;
-      px = q - div_small(q, nv, inv_nv) * nv;
+      pxd = (q - int(__umulhi(uint32_t(q) << 1, m_nv)) * nv) << 24;
       T = mk(1.f, 1.f, 1.f);
-      depth = 0;
     } else {
       active = false;
     }
@@ -462,14 +470,14 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   for (;;) {
     const unsigned long long live = __ballot(active);
     if (live == 0) break;
-    nseg += unsigned(__popcll(live));
+    nseg = unsigned(__builtin_amdgcn_readfirstlane(int(nseg + unsigned(__popcll(live)))));
     bool done = false;
     V3<float> col = mk(0.f, 0.f, 0.f);
 #if RTMI_TRACE_PHASES
     const unsigned long long cyc_a = __builtin_amdgcn_s_memtime();
 #endif
     if (active) {
-      done = path_segment<ACC>(sc, pairs, a, o, d, T, depth, rng, col, cnt, segments);
+      done = path_segment<ACC>(sc, pairs, a, o, d, T, pxd, rng, col, cnt, segments);
     }
 #if RTMI_TRACE_PHASES
     const unsigned long long cyc_b = __builtin_amdgcn_s_memtime();
@@ -483,6 +491,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
     const unsigned long long m = __ballot(done);
     if (m) {
       if (done) {
+        const int px = pxd >> 24;
         atomicAdd(&acc[wave][0][px], (unsigned long long)to_fixed(col.x));
         atomicAdd(&acc[wave][1][px], (unsigned long long)to_fixed(col.y));
         atomicAdd(&acc[wave][2][px], (unsigned long long)to_fixed(col.z));
@@ -495,7 +504,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
       const int cnt = __popcll(m);
       for (int served = 0; served < cnt;) {
         if (ppos == 64) {
-          pbase += 64;
+          pbase = __builtin_amdgcn_readfirstlane(pbase + 64);
           ppos = 0;
           if (pbase < nq) camera_ray(pbase + lane, po, pd, prng);
         }
@@ -509,8 +518,8 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
         g.s0 = pull64(src4, prng.s0);
         g.s1 = pull64(src4, prng.s1);
         if (done && r >= 0 && r < take) adopt(pbase + ppos + r, ro, rd, g);
-        ppos += take;
-        served += take;
+        ppos = __builtin_amdgcn_readfirstlane(ppos + take);
+        served = __builtin_amdgcn_readfirstlane(served + take);
       }
 #else
       if (done) {
@@ -545,16 +554,20 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   if (lane == 0) { atomicAdd(&segments[4], cyc_iter); atomicAdd(&segments[7], cyc_regen); }
 #endif
   RTMI_TRACE_END(1, nseg)
+  // the lane index recomputed here, not kept live (in scratch) since the
+  // accumulator's initialisation
+  int fl = int(threadIdx.x & 63u);
+  asm volatile("" : "+v"(fl));
   if constexpr (CHUNKED) {
     if (a.block_flush) {  // block-uniform; no wave of this block returned early
       __syncthreads();
-      if (wave == 0 && lane < nv) {
-        const int ly = lane / vw, lx = lane - ly * vw;
+      if (wave == 0 && fl < nv) {
+        const int ly = fl / vw, lx = fl - ly * vw;
         const size_t o3 = (size_t(y0 + ly) * size_t(a.W) + size_t(x0 + lx)) * 3;
         for (int c = 0; c < 3; ++c) {
           unsigned long long v = 0;
 #pragma unroll
-          for (int w = 0; w < WPB; ++w) v += acc[w][c][lane];
+          for (int w = 0; w < WPB; ++w) v += acc[w][c][fl];
           if (a.block_owns_tile) out[o3 + c] = from_fixed((long long)v);
           else atomicAdd(&accum[o3 + c], v);
         }
@@ -562,8 +575,8 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
       return;
     }
   }
-  if (lane < nv) {
-    const int ly = lane / vw, lx = lane - ly * vw;
+  if (fl < nv) {
+    const int ly = fl / vw, lx = fl - ly * vw;
     const size_t o3 = (size_t(y0 + ly) * size_t(a.W) + size_t(x0 + lx)) * 3;
 #if RTMI_CHECK
     if (o3 + 3 > a.out_elems) {
@@ -572,7 +585,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
     } else
 #endif
     for (int c = 0; c < 3; ++c) {
-      const unsigned long long v = acc[wave][c][lane];
+      const unsigned long long v = acc[wave][c][fl];
       if constexpr (CHUNKED) atomicAdd(&accum[o3 + c], v);
       else out[o3 + c] = from_fixed((long long)v);
     }
@@ -1041,7 +1054,7 @@ int check_render_args(const rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_
   if (!ctx || !cam) return set_error(RT_EINVAL, "null context or camera");
   if (W < 2 || H < 2) return set_error(RT_EINVAL, "image must be at least 2x2 (u,v divide by W-1, H-1)");
   if (spp < 1 || spp >= (1 << 24)) return set_error(RT_EINVAL, "spp must be in [1, 2^24)");
-  if (max_depth < 0) return set_error(RT_EINVAL, "max_depth must be >= 0");
+  if (max_depth < 0 || max_depth >= (1 << 24)) return set_error(RT_EINVAL, "max_depth must be in [0, 2^24)");
   if (int64_t(W) * int64_t(H) >= (int64_t(1) << 40)) return set_error(RT_EINVAL, "image too large");
   if (ctx->n <= 0) return set_error(RT_EINVAL, "no scene uploaded (rt_ctx_set_scene)");
   return RT_OK;

@@ -171,7 +171,9 @@ int rt_ctx_accel_info(rt_ctx *ctx, int32_t *n_big, int32_t *n_nodes);
 int rt_ctx_grid_info(rt_ctx *ctx, int32_t *dims3, int32_t *n_refs, int32_t *lds_bytes);
 
 /* The whole image: replaces the 16-thread worker() block main.cpp:313-338.
- * Synchronous; `sum` is a HOST buffer of W*H*3 floats. */
+ * Synchronous; `sum` is a HOST buffer of W*H*3 floats.  max_depth is in
+ * [0, 2^24) (RT_EINVAL otherwise; the reference's recursion would exhaust its
+ * stack long before). */
 int rt_render(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t spp,
               int32_t max_depth, uint64_t seed, float *sum);
 

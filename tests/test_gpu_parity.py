@@ -747,3 +747,15 @@ def test_exact_math_exhaustive(which):
     v = (C.c_uint64 * 4)()
     rt.check(f(which, v), "rt_debug_exact_math")
     assert v[0] == 0, f"{v[0]} mismatches; first input {v[1]:#010x}: got {v[2]:#010x}, IEEE {v[3]:#010x}"
+
+
+def test_max_depth_range(final_renderer):
+    """max_depth must lie in [0, 2^24): the kernels keep a path's depth in 24
+    bits (its pixel above them).  The largest value renders like any deep
+    limit (every path ends long before it); 2^24 is rejected."""
+    cam = rt.final_camera(16 / 8)
+    deep = final_renderer.render(cam, 16, 8, 4, (1 << 24) - 1, SEED)
+    assert np.array_equal(deep, final_renderer.render(cam, 16, 8, 4, 100000, SEED))
+    with pytest.raises(rt.RTError) as e:
+        final_renderer.render(cam, 16, 8, 4, 1 << 24, SEED)
+    assert "RT_EINVAL" in str(e.value)

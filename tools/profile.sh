@@ -5,7 +5,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-OUT=gpurun_out/prof_${TAG:-r02}
+OUT=gpurun_out/${TAG:-prof_r02}
 mkdir -p $OUT
 B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-exec-counts --timed-only $BENCH_ARGS"
 echo "== kernel trace"

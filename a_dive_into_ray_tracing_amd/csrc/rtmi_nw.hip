@@ -194,11 +194,20 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
   float time = 0.f;
   int px = 0, depth = 0;
   Xoro rng;
-  // job q -> pixel q % nv, sample s0 + q / nv; camera ray main.cu:139-141
+  // job q -> pixel q % nv, sample s0 + q / nv; camera ray main.cu:139-141.
+  // Grid kernels: q / d = umulhi(2q, ceil(2^31 / d)), exact for d <= 64,
+  // q < 2^25 (the RTIOW kernel's job decode, tests/test_kernel_arith.py;
+  // chunk <= 65535 keeps q < 2^22) — a multiply instead of the 32-bit division
+  // expansion (motion blur 59.5 -> 58.1 ms); the BVH kernel keeps the division
+  // (its two multipliers cost more registers than they save: final scene
+  // 283.6 -> 286.2 ms at 256 spp, profiles/r03/ab_nw_jobdiv.txt)
+  constexpr bool kMulDiv = GRID;
+  const uint32_t m_nv = 0x7FFFFFFFu / uint32_t(max(nv, 1)) + 1u, m_vw = 0x7FFFFFFFu / uint32_t(vw) + 1u;
   auto start = [&](int q) {
-    const int s = s0 + q / nv;
-    px = q - (q / nv) * nv;
-    const int ly = px / vw, lx = px - ly * vw;
+    const int qs = kMulDiv ? int(__umulhi(uint32_t(q) << 1, m_nv)) : q / nv;
+    const int s = s0 + qs;
+    px = q - qs * nv;
+    const int ly = kMulDiv ? int(__umulhi(uint32_t(px) << 1, m_vw)) : px / vw, lx = px - ly * vw;
     const int i = x0 + lx;
     const int j = a.row0 + (y0 + ly) * a.row_step;
     rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(s));
@@ -857,7 +866,9 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
     const int64_t waves = int64_t(resident) * pwaves;
     chunk = std::min<int64_t>(32, std::max<int64_t>(4, int64_t(a.tiles) * spp / (80 * waves)));
   }
-  a.chunk = std::min<int64_t>(spp, ctx->env_chunk > 0 ? ctx->env_chunk : chunk);
+  // (at most 65535 samples per item: job indices stay below 2^22, where the
+  // kernels' reciprocal-multiply job decode is exact)
+  a.chunk = std::min<int64_t>({spp, ctx->env_chunk > 0 ? ctx->env_chunk : chunk, 65535});
   a.nch = (spp + a.chunk - 1) / a.chunk;
   if (int64_t(a.tiles) * a.nch >= (int64_t(1) << 31) - kWaves) return set_error(RT_EINVAL, "render too large");
   a.n_items = a.tiles * a.nch;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 3, pass c: the whole record of the current tree in one GPU call —
+# Round 3, pass c (B=<name> for later passes): the whole record of the current tree in one GPU call —
 # smoke + GPU suite + bench line + 1/8 strip + rocprofv3 kernel trace
 # (gpu_pass.sh), PMC passes (profile.sh), the write budget passes
 # (gpu_r03_writes.sh), configs 4 and 5 (gpu_r03_workloads.sh) and the
@@ -7,7 +7,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-B=r03c_pass
+B=${B:-r03c_pass}
 TAG=$B/pass bash tools/gpu_pass.sh || exit 1
 TAG=$B/prof bash tools/profile.sh > gpurun_out/$B/profile.log 2>&1 || { tail -5 gpurun_out/$B/profile.log; exit 1; }
 tail -3 gpurun_out/$B/profile.log

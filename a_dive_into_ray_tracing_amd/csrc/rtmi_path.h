@@ -51,21 +51,44 @@ template <bool F> __device__ __forceinline__ double madd(double a, double b, dou
 #ifndef RTMI_EXACT_MATH
 #define RTMI_EXACT_MATH 1
 #endif
+// (The out-of-range inputs take the IEEE form behind a wave-uniform branch on
+// their ballot: the common path pays one compare and a scalar branch, not an
+// exec-mask save/restore.)
+#ifndef RTMI_MATH_UNIFORM_GUARD
+#define RTMI_MATH_UNIFORM_GUARD 1
+#endif
 __device__ __forceinline__ float sqrt_cr(float x) {
   // below 2^-96 (zero, denormals — which v_sqrt_f32 flushes — negatives,
   // NaN) the residuals would underflow: the IEEE lowering
-  if (!(x >= 0x1p-96f)) return __builtin_sqrtf(x);
+  const bool slow = !(x >= 0x1p-96f);
+#if !RTMI_MATH_UNIFORM_GUARD
+  if (slow) return __builtin_sqrtf(x);
+#endif
   const float s = __builtin_amdgcn_sqrtf(x);
   const float sm = __int_as_float(__float_as_int(s) - 1), sp = __int_as_float(__float_as_int(s) + 1);
   float r = __builtin_fmaf(-sm, s, x) <= 0.0f ? sm : s;
   r = __builtin_fmaf(-sp, s, x) > 0.0f ? sp : r;
+#if RTMI_MATH_UNIFORM_GUARD
+  if (__builtin_expect(__ballot(slow) != 0, 0)) {
+    if (slow) r = __builtin_sqrtf(x);
+  }
+#endif
   return r;
 }
 __device__ __forceinline__ float rcp_cr(float x) {
   const float ax = __builtin_fabsf(x);
-  if (!(ax >= 0x1p-125f && ax <= 0x1p+125f)) return 1.0f / x;  // zero, denormal, huge, inf, NaN
-  const float r = __builtin_amdgcn_rcpf(x);
-  return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+  const bool slow = !(ax >= 0x1p-125f && ax <= 0x1p+125f);  // zero, denormal, huge, inf, NaN
+#if !RTMI_MATH_UNIFORM_GUARD
+  if (slow) return 1.0f / x;
+#endif
+  const float r0 = __builtin_amdgcn_rcpf(x);
+  float r = __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
+#if RTMI_MATH_UNIFORM_GUARD
+  if (__builtin_expect(__ballot(slow) != 0, 0)) {
+    if (slow) r = 1.0f / x;
+  }
+#endif
+  return r;
 }
 #if RTMI_EXACT_MATH
 __device__ __forceinline__ float dsqrt(float x) { return sqrt_cr(x); }

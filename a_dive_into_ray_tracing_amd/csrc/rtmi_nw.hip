@@ -192,7 +192,9 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
 
   V o, d, T;
   float time = 0.f;
-  int px = 0, depth = 0;
+  // the path's pixel in the tile (bits 24..29) and its depth (bits 0..23;
+  // max_depth < 2^24 is checked on the host) in one register
+  int pxd = 0;
   Xoro rng;
   // job q -> pixel q % nv, sample s0 + q / nv; camera ray main.cu:139-141.
   // Grid kernels: q / d = umulhi(2q, ceil(2^31 / d)), exact for d <= 64,
@@ -206,7 +208,7 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
   auto start = [&](int q) {
     const int qs = kMulDiv ? int(__umulhi(uint32_t(q) << 1, m_nv)) : q / nv;
     const int s = s0 + qs;
-    px = q - qs * nv;
+    const int px = q - qs * nv;
     const int ly = kMulDiv ? int(__umulhi(uint32_t(px) << 1, m_vw)) : px / vw, lx = px - ly * vw;
     const int i = x0 + lx;
     const int j = a.row0 + (y0 + ly) * a.row_step;
@@ -227,7 +229,7 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
     get_ray<true, float>(cm, u, v, rng, o, d);
     time = __builtin_fmaf(rng.uni(), cl[20], cl[19]);  // camera.h:75-79
     T = mk(1.f, 1.f, 1.f);
-    depth = 0;
+    pxd = px << 24;
   };
 
 #if RTMI_NW_PHASES
@@ -239,14 +241,15 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
   if (active) start(lane);
   int next = 64;
   for (;;) {
-    if (__ballot(active) == 0) break;
+    const unsigned long long live = __ballot(active);
+    if (live == 0) break;
+    nseg = unsigned(__builtin_amdgcn_readfirstlane(int(nseg + unsigned(__popcll(live)))));
     bool done = false;
     V col = mk(0.f, 0.f, 0.f);
 #if RTMI_NW_PHASES
     pa = __builtin_amdgcn_s_memtime();
 #endif
     if (active) {
-      ++nseg;
       const uint64_t seg_key = !S && sc.has_media ? rng.next() : 0ull;
       float t;
       int face;
@@ -272,7 +275,7 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
           T = mul3(T, at);
           o = rec.p;
           d = nd;
-          if (++depth >= a.max_depth) {  // main.cu:100: the background, unattenuated
+          if ((++pxd & 0xFFFFFF) >= a.max_depth) {  // main.cu:100: the background, unattenuated
             col = mk(sc.bg[0], sc.bg[1], sc.bg[2]);
             done = true;
           }
@@ -288,6 +291,7 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
     const unsigned long long m = __ballot(done);
     if (m) {
       if (done) {
+        const int px = pxd >> 24;
         atomicAdd(&acc[0][px], (unsigned long long)fixed(col.x));
         atomicAdd(&acc[1][px], (unsigned long long)fixed(col.y));
         atomicAdd(&acc[2][px], (unsigned long long)fixed(col.z));
@@ -296,7 +300,7 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
         if (q < nq) start(q);
         else active = false;
       }
-      next += __popcll(m);
+      next = __builtin_amdgcn_readfirstlane(next + int(__popcll(m)));
     }
 #if RTMI_NW_PHASES
     ph[2] += __builtin_amdgcn_s_memtime() - pc;
@@ -331,9 +335,7 @@ __device__ __forceinline__ void run_item(const View &sc, const Args &a, int item
 }
 
 __device__ __forceinline__ void add_segments(unsigned nseg, int lane, unsigned long long *segments) {
-  unsigned long long ws = nseg;  // wave sum of the lanes' world.hit calls -> one atomic
-  for (int off = 32; off > 0; off >>= 1) ws += __shfl_xor(ws, off);
-  if (lane == 0) atomicAdd(segments, ws);
+  if (lane == 0) atomicAdd(segments, (unsigned long long)nseg);  // the wave's world.hit calls (wave-uniform)
 }
 
 template <bool CHUNKED, bool LDS_NODES, bool LDS_OBJS, bool GRID>
@@ -768,8 +770,9 @@ RTMI_EXPORT int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
                                   float *dev_strip, void *stream) {
   if (!ctx || !cam || !dev_strip) return set_error(RT_EINVAL, "rt_nw_render_rows: null argument");
   if (ctx->nobj + ctx->nmed <= 0) return set_error(RT_EINVAL, "no scene uploaded (rt_nw_ctx_set_scene)");
-  if (W < 1 || H < 1 || spp < 1 || spp >= (1 << 24) || max_depth < 1 || int64_t(W) * H >= (int64_t(1) << 40))
-    return set_error(RT_EINVAL, "rt_nw_render_rows: bad size (W, H, spp >= 1, spp < 2^24, max_depth >= 1)");
+  if (W < 1 || H < 1 || spp < 1 || spp >= (1 << 24) || max_depth < 1 || max_depth >= (1 << 24) ||
+      int64_t(W) * H >= (int64_t(1) << 40))
+    return set_error(RT_EINVAL, "rt_nw_render_rows: bad size (W, H, spp >= 1, spp < 2^24, 1 <= max_depth < 2^24)");
   if (nrows < 1 || row_step < 1 || row0 < 0 || row0 >= H) return set_error(RT_EINVAL, "rt_nw_render_rows: bad row set");
   if (!(cam->time0 >= 0.0 && cam->time1 <= 1.0 && cam->time0 <= cam->time1))
     return set_error(RT_EINVAL, "rt_nw_render_rows: shutter must lie in [0, 1]");

@@ -122,12 +122,6 @@ __device__ unsigned g_trace_n;
 #ifndef RTMI_CHECK
 #define RTMI_CHECK 0
 #endif
-// render_kernel's camera-ray pool; 0: each lane generates
-// its next camera ray itself when its path ends (analysis / A-B builds)
-#ifndef RTMI_RAY_POOL
-#define RTMI_RAY_POOL 1
-#endif
-constexpr int kRayPool = RTMI_RAY_POOL;
 #ifndef RTMI_PERSIST_MIN_BLOCKS
 #define RTMI_PERSIST_MIN_BLOCKS 1
 #endif
@@ -438,7 +432,6 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
     }
   };
 
-#if RTMI_RAY_POOL
   // Camera-ray pool: lane L holds the camera ray of job
   // pbase + L, generated by all 64 lanes at once; a lane whose path ended
   // takes the next unused slot through ds_bpermute.  The ray generation runs
@@ -455,17 +448,6 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
     const uint32_t hi = uint32_t(__builtin_amdgcn_ds_bpermute(src4, int(uint32_t(v >> 32))));
     return (uint64_t(hi) << 32) | lo;
   };
-#else
-  if (lane < nq) {
-    V3<float> ro, rd;
-    Xoro g;
-    camera_ray(lane, ro, rd, g);
-    adopt(lane, ro, rd, g);
-  } else {
-    active = false;
-  }
-  int next = 64;
-#endif
 
   for (;;) {
     const unsigned long long live = __ballot(active);
@@ -482,11 +464,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
 #if RTMI_TRACE_PHASES
     const unsigned long long cyc_b = __builtin_amdgcn_s_memtime();
     cyc_iter += cyc_b - cyc_a;  // hit + shading of this pass (wave-level)
-#if RTMI_RAY_POOL
     const bool ramp = pbase + 64 >= nq && ppos == 64;  // the item's jobs all taken: the wave's ramp-down
-#else
-    const bool ramp = next >= nq;
-#endif
 #endif
     const unsigned long long m = __ballot(done);
     if (m) {
@@ -497,7 +475,6 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
         atomicAdd(&acc[wave][2][px], (unsigned long long)to_fixed(col.z));
       }
       const int rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
-#if RTMI_RAY_POOL
       // ranks [0, cnt) take slots ppos, ppos + 1, ...: at most two rounds,
       // the second after a refill for the next 64 jobs (skipped once the
       // item has none: those lanes go idle)
@@ -521,16 +498,6 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
         ppos = __builtin_amdgcn_readfirstlane(ppos + take);
         served = __builtin_amdgcn_readfirstlane(served + take);
       }
-#else
-      if (done) {
-        const int q = next + rank;
-        V3<float> ro, rd;
-        Xoro g;
-        if (q < nq) camera_ray(q, ro, rd, g);
-        adopt(q, ro, rd, g);
-      }
-      next += __popcll(m);
-#endif
     }
 #if RTMI_TRACE_PHASES
     const unsigned long long cyc_e = __builtin_amdgcn_s_memtime();
@@ -1690,7 +1657,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   a.block_owns_tile = a.block_flush && !pass_accum && nch1 == grid_wpb && nch2 == 0 && ctx->block_owns;
   const bool chunked = pass_accum || nch1 + nch2 > 1;
   if (!ctx->probing) {
-    const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush + a.block_owns_tile, persistent ? 0 : kRayPool, persistent ? 1 : 0,
+    const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush + a.block_owns_tile, persistent ? 0 : 1, persistent ? 1 : 0,
                               acc_kind == 3 ? 2 : acc_kind};
     std::copy(sched, sched + 8, ctx->last_sched);
   }

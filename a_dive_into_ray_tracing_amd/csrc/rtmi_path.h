@@ -48,55 +48,34 @@ template <bool F> __device__ __forceinline__ double madd(double a, double b, dou
 //  reciprocal: v_rcp_f32, then one Newton step with exact fma residual; the
 //  ranges where 1/x or x lies outside the normal range keep the IEEE
 //  division (a branch no realistic scene takes).
-#ifndef RTMI_EXACT_MATH
-#define RTMI_EXACT_MATH 1
-#endif
 // (The out-of-range inputs take the IEEE form behind a wave-uniform branch on
 // their ballot: the common path pays one compare and a scalar branch, not an
-// exec-mask save/restore.)
-#ifndef RTMI_MATH_UNIFORM_GUARD
-#define RTMI_MATH_UNIFORM_GUARD 1
-#endif
+// exec-mask save/restore — DESIGN.md §4.6.)
 __device__ __forceinline__ float sqrt_cr(float x) {
   // below 2^-96 (zero, denormals — which v_sqrt_f32 flushes — negatives,
   // NaN) the residuals would underflow: the IEEE lowering
   const bool slow = !(x >= 0x1p-96f);
-#if !RTMI_MATH_UNIFORM_GUARD
-  if (slow) return __builtin_sqrtf(x);
-#endif
   const float s = __builtin_amdgcn_sqrtf(x);
   const float sm = __int_as_float(__float_as_int(s) - 1), sp = __int_as_float(__float_as_int(s) + 1);
   float r = __builtin_fmaf(-sm, s, x) <= 0.0f ? sm : s;
   r = __builtin_fmaf(-sp, s, x) > 0.0f ? sp : r;
-#if RTMI_MATH_UNIFORM_GUARD
   if (__builtin_expect(__ballot(slow) != 0, 0)) {
     if (slow) r = __builtin_sqrtf(x);
   }
-#endif
   return r;
 }
 __device__ __forceinline__ float rcp_cr(float x) {
   const float ax = __builtin_fabsf(x);
   const bool slow = !(ax >= 0x1p-125f && ax <= 0x1p+125f);  // zero, denormal, huge, inf, NaN
-#if !RTMI_MATH_UNIFORM_GUARD
-  if (slow) return 1.0f / x;
-#endif
   const float r0 = __builtin_amdgcn_rcpf(x);
   float r = __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
-#if RTMI_MATH_UNIFORM_GUARD
   if (__builtin_expect(__ballot(slow) != 0, 0)) {
     if (slow) r = 1.0f / x;
   }
-#endif
   return r;
 }
-#if RTMI_EXACT_MATH
 __device__ __forceinline__ float dsqrt(float x) { return sqrt_cr(x); }
 __device__ __forceinline__ float drcp(float x) { return rcp_cr(x); }
-#else
-__device__ __forceinline__ float dsqrt(float x) { return __builtin_sqrtf(x); }
-__device__ __forceinline__ float drcp(float x) { return 1.0f / x; }
-#endif
 __device__ __forceinline__ double dsqrt(double x) { return __builtin_sqrt(x); }
 __device__ __forceinline__ double drcp(double x) { return 1.0 / x; }
 __device__ __forceinline__ float dfabs(float x) { return __builtin_fabsf(x); }
@@ -570,6 +549,7 @@ __device__ __forceinline__ float safe_inv(float v) {
 #define RTMI_TRACE_PHASES 0
 #endif
 
+
 #if RTMI_TRACE_PHASES
 // analysis only: wave-level cycles (s_memtime) of the grid walk's phases:
 // [0] big spheres, [1] clip + DDA setup, [2] cell walk
@@ -778,6 +758,21 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
         }
       }
       const float texit = __builtin_fminf(tnx, __builtin_fminf(tny, tnz));
+      if constexpr (FLAT_Y) {
+        // the same step without nested branches: x when its face is nearest
+        // (ties to x), the y face ends the walk, else z (selects: 19.92 vs
+        // 20.06 ms, profiles/r03/ab_dda_select_shade_uniform.txt)
+        const bool sx = (tnx <= tny) & (tnx <= tnz);
+        const bool sy = !sx & (tny <= tnz);
+        const bool leave = !(texit < t_max) | sy | ((sx ? kx : kz) >= (sx ? kmx : kmz));
+        if (leave) break;
+        kx = sx ? kx + 1.0f : kx;
+        kz = sx ? kz : kz + 1.0f;
+        tnx = sx ? __builtin_fmaf(kx, dtx, t0x) : tnx;
+        tnz = sx ? tnz : __builtin_fmaf(kz, dtz, t0z);
+        cell += sx ? dcx : dcz;
+        continue;
+      }
       if (!(texit < t_max)) break;  // the closest hit so far lies in the cells walked
       if (tnx <= tny && tnx <= tnz) {
         if (kx >= kmx) break;  // leaves the grid

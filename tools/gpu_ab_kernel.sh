@@ -1,6 +1,7 @@
 #!/bin/bash
 # Kernel-shape A/B on the 1/8 strip and the frame (grid accel): one wave per
-# item (grid kernel), the persistent kernel, the block job pool
+# item (grid kernel), the persistent kernel (round 2; its block-job-pool leg
+# was dropped with the pool in round 3)
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/${TAG:-ab_kernel}; mkdir -p $OUT
 run() {  # name env... -- bench args
@@ -11,6 +12,5 @@ run() {  # name env... -- bench args
 for rep in 1 2; do
   EXTRA="--strip-of 8" run s8_grid_$rep X=1
   EXTRA="--strip-of 8 --kernel persistent" run s8_pers_$rep X=1
-  EXTRA="--strip-of 8" run s8_pool_$rep RTMI_BLOCK_POOL=1
   EXTRA="--kernel persistent" run f_pers_$rep X=1
 done

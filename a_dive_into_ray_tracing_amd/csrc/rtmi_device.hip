@@ -307,7 +307,11 @@ __device__ __forceinline__ bool path_segment(const SceneView<float> &sc, const S
   // the hit sphere's three records in one memory round trip (a miss reads
   // sphere 0's, unused)
   const int kk = miss ? 0 : k;
-  const float4 sh1k = sc.sh1[kk], sh0k = sc.sh0[kk], geomk = sc.geom[kk];
+  // the grid kernels hold every sphere's {c, S} in LDS at its scene index
+  // (stage_grid): the hit record's geometry from there, one global gather
+  // fewer (19.82 -> 19.73 ms, profiles/r03/ab_geom_lds.txt)
+  const float4 sh1k = sc.sh1[kk], sh0k = sc.sh0[kk];
+  const float4 geomk = ACC >= 2 ? lds_sphere(lds_address(rtmi_bvh_lds) + 16u * uint32_t(kk)) : sc.geom[kk];
   const int kind = miss ? -1 : int(sh1k.x);
   float inv_len = 0.0f;
   if (kind != RT_MAT_LAMBERTIAN) inv_len = drcp(dsqrt(dot<true>(d, d)));

@@ -67,6 +67,20 @@ void destroy(rt_multi *m) {
   delete m;
 }
 
+// After a failure part-way through a multi-device call, some devices' streams
+// may still hold enqueued work (strips, passes, a gather) that reads or writes
+// this object's buffers and records its events: wait for all of it before
+// returning the error, so the next call (or rt_multi_destroy) starts from idle
+// devices.  Errors here are ignored: the call is already failing.
+int drain(rt_multi *m, int rc) {
+  for (int g = 0; g < int(m->ctx.size()); g++)
+    if (m->ctx[g]) {
+      (void)hipSetDevice(g);
+      (void)hipStreamSynchronize(rtmi::ctx_stream(m->ctx[g]));
+    }
+  return rc;
+}
+
 struct KeepDevice {
   int prev = 0;
   KeepDevice() { (void)hipGetDevice(&prev); }
@@ -102,7 +116,7 @@ int ensure_buffers(rt_multi *m, size_t strip_elems) {
 
 // The single exchange step: every strip (already enqueued on its device's
 // stream) to GPU 0, then rows un-permuted into the host image.
-int gather_unpermute(rt_multi *m, int32_t W, int32_t H, int32_t nrows, float *sum) {
+int gather_unpermute_body(rt_multi *m, int32_t W, int32_t H, int32_t nrows, float *sum) {
   const int G = m->G;
   const size_t strip_elems = size_t(nrows) * W * 3;
   std::vector<hipStream_t> streams(G);
@@ -141,6 +155,10 @@ int gather_unpermute(rt_multi *m, int32_t W, int32_t H, int32_t nrows, float *su
   if (hipMemcpy(m->host.data(), m->recv, m->host.size() * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
     return set_error(RT_EHIP, "gather buffer copy");
   return rt_unpermute_rows(m->host.data(), G, nrows, W, H, sum);
+}
+int gather_unpermute(rt_multi *m, int32_t W, int32_t H, int32_t nrows, float *sum) {
+  const int rc = gather_unpermute_body(m, W, H, nrows, sum);
+  return rc == RT_OK ? rc : drain(m, rc);
 }
 }  // namespace
 
@@ -223,8 +241,8 @@ RTMI_EXPORT int rt_multi_render(rt_multi *m, const rt_camera *cam, int32_t W, in
     (void)hipSetDevice(g);
     if (rc == RT_OK && hipEventRecord(m->ev_end[g], s) != hipSuccess) rc = set_error(RT_EHIP, "event on GPU %d", g);
   }
-  if (rc == RT_OK) rc = gather_unpermute(m, W, H, nrows, sum);
-  return rc;
+  if (rc != RT_OK) return drain(m, rc);  // earlier devices' strips may be in flight
+  return gather_unpermute(m, W, H, nrows, sum);
 }
 
 RTMI_EXPORT int rt_multi_last_timing(rt_multi *m, float *strip_ms, float *gather_ms) {
@@ -239,8 +257,9 @@ RTMI_EXPORT int rt_multi_accum_reset(rt_multi *m, int32_t W, int32_t H) {
   if (!m || W < 2 || H < 2) return set_error(RT_EINVAL, "rt_multi_accum_reset: bad argument");
   KeepDevice keep;
   const int32_t nrows = (H + m->G - 1) / m->G;
+  m->pass_W = 0;  // no valid accumulator set until every device has reset its own
   for (int g = 0; g < m->G; g++)
-    if (int rc = rt_accum_reset(m->ctx[g], W, nrows)) return rc;
+    if (int rc = rt_accum_reset(m->ctx[g], W, nrows)) return drain(m, rc);
   m->pass_W = W;
   m->pass_H = H;
   m->pass_nrows = nrows;
@@ -252,15 +271,23 @@ RTMI_EXPORT int rt_multi_render_pass(rt_multi *m, const rt_camera *cam, int32_t 
   if (!m || !cam) return set_error(RT_EINVAL, "rt_multi_render_pass: bad argument");
   if (!m->pass_W) return set_error(RT_EINVAL, "rt_multi_render_pass: no accumulator (rt_multi_accum_reset)");
   KeepDevice keep;
-  for (int g = 0; g < m->G; g++) {
+  int rc = RT_OK;
+  for (int g = 0; g < m->G && rc == RT_OK; g++) {
     (void)hipSetDevice(g);
     hipStream_t s = rtmi::ctx_stream(m->ctx[g]);
-    if (hipEventRecord(m->ev_begin[g], s) != hipSuccess) return set_error(RT_EHIP, "event on GPU %d", g);
-    if (int rc = rt_render_pass(m->ctx[g], cam, m->pass_W, m->pass_H, s_begin, s_count, max_depth, seed, g, m->G,
-                                m->pass_nrows, nullptr))
-      return rc;
+    if (hipEventRecord(m->ev_begin[g], s) != hipSuccess) rc = set_error(RT_EHIP, "event on GPU %d", g);
+    if (rc == RT_OK)
+      rc = rt_render_pass(m->ctx[g], cam, m->pass_W, m->pass_H, s_begin, s_count, max_depth, seed, g, m->G,
+                          m->pass_nrows, nullptr);
     (void)hipSetDevice(g);
-    if (hipEventRecord(m->ev_end[g], s) != hipSuccess) return set_error(RT_EHIP, "event on GPU %d", g);
+    if (rc == RT_OK && hipEventRecord(m->ev_end[g], s) != hipSuccess) rc = set_error(RT_EHIP, "event on GPU %d", g);
+  }
+  if (rc != RT_OK) {
+    // devices 0..g-1 hold this pass's samples and the others do not: the
+    // accumulators no longer cover one sample range, so resolving them would
+    // return rows of different sample counts.  Invalid until the next reset.
+    m->pass_W = 0;
+    return drain(m, rc);
   }
   return RT_OK;
 }
@@ -278,8 +305,8 @@ RTMI_EXPORT int rt_multi_accum_resolve(rt_multi *m, float *sum) {
     (void)hipSetDevice(g);
     if (rc == RT_OK && hipEventRecord(m->ev_end[g], s) != hipSuccess) rc = set_error(RT_EHIP, "event on GPU %d", g);
   }
-  if (rc == RT_OK) rc = gather_unpermute(m, m->pass_W, m->pass_H, m->pass_nrows, sum);
-  return rc;
+  if (rc != RT_OK) return drain(m, rc);
+  return gather_unpermute(m, m->pass_W, m->pass_H, m->pass_nrows, sum);
 }
 
 RTMI_EXPORT int rt_render_multi(const rt_scene *scene, const rt_camera *cam, int32_t W, int32_t H, int32_t spp,

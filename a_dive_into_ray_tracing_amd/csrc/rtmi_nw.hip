@@ -395,11 +395,14 @@ __global__ void trace_kernel(View sc, Args a, int i, int j, int s, float *rec, i
   get_ray<true, float>(a.cam, (float(i) + ju) / float(a.W), (float(j) + jv) / float(a.H), rng, o, d);
   const float time = __builtin_fmaf(rng.uni(), a.time1 - a.time0, a.time0);
   int n = 0;
+  // the walk's work counters (written only by the RTMI_STATS build, which
+  // would otherwise dereference a null counter pointer here)
+  NwCount tcnt{0, 0, 0, 0};
   for (int depth = 0; depth < a.max_depth && n < cap; ++depth) {
     const uint64_t seg_key = sc.has_media ? rng.next() : 0ull;
     float t;
     int face;
-    const int32_t k = hit_world_nw<false, false>(sc, o, d, time, seg_key, t, face);
+    const int32_t k = hit_world_nw<false, false>(sc, o, d, time, seg_key, t, face, &tcnt);
     float *r = rec + 12 * n++;
     r[0] = o.x; r[1] = o.y; r[2] = o.z; r[3] = d.x; r[4] = d.y; r[5] = d.z; r[6] = t;
     r[7] = __int_as_float(k < 0 ? -1 : k < sc.nobj ? sc.obj_id[k] : sc.med_id[k - sc.nobj]);

@@ -418,7 +418,7 @@ __device__ __forceinline__ bool hit_object(const View &sc, const DevObj &ob, V o
 extern __shared__ float4 nw_nodes_lds[];
 template <bool LDS_NODES, bool LDS_OBJS>
 __device__ __forceinline__ int32_t hit_world_nw(const View &sc, V o, V d, float time, uint64_t seg_key, float &best_t,
-                                                int &best_face, NwCount *cnt = nullptr) {
+                                                int &best_face, NwCount *cnt) {
   const float4 *nlo = LDS_NODES ? nw_nodes_lds : sc.nlo;
   const float4 *nhi = LDS_NODES ? nw_nodes_lds + sc.nnodes : sc.nhi;
   const DevObj *objs = LDS_OBJS ? reinterpret_cast<const DevObj *>(nw_nodes_lds + 2 * sc.nnodes) : sc.obj;
@@ -510,7 +510,7 @@ __host__ __device__ constexpr size_t nw_grid_lds_bytes(int32_t nobj, int32_t nce
 // whole shutter (moving spheres) and the composed transform (instances).
 template <bool S = false>
 __device__ __forceinline__ int32_t hit_world_nw_grid(const View &sc, V o, V d, float time, uint64_t seg_key,
-                                                     float &best_t, int &best_face, NwCount *cnt = nullptr) {
+                                                     float &best_t, int &best_face, NwCount *cnt) {
   const DevObj *objs = reinterpret_cast<const DevObj *>(nw_nodes_lds);
   const int32_t *oids = reinterpret_cast<const int32_t *>(nw_nodes_lds + 3 * sc.nobj);
   const uint16_t *cs = reinterpret_cast<const uint16_t *>(oids + sc.nobj);
@@ -579,7 +579,8 @@ __device__ __forceinline__ int32_t hit_world_nw_grid(const View &sc, V o, V d, f
     int cx = cell_of(__builtin_fmaf(tnear, d.x, o.x), 0);
     int cy = cell_of(__builtin_fmaf(tnear, d.y, o.y), 1);
     int cz = cell_of(__builtin_fmaf(tnear, d.z, o.z), 2);
-    const int sx = d.x >= 0.0f ? 1 : -1, sy = d.y >= 0.0f ? 1 : -1, sz = d.z >= 0.0f ? 1 : -1;
+    // step signs from the culling inverses (safe_inv maps -0.0 to -1e20)
+    const int sx = ix >= 0.0f ? 1 : -1, sy = iy >= 0.0f ? 1 : -1, sz = iz >= 0.0f ? 1 : -1;
     auto tface = [&](int c, int s, int ax, float inv, float oo) {
       return __builtin_fmaf(__builtin_fmaf(float(c + (s > 0)), G.h[ax], G.g0[ax]), inv, oo);
     };

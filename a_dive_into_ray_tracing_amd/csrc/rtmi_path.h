@@ -714,25 +714,28 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
     // §4.5's argument needs face parameters within ~1e-6 of the truth, the
     // margins being >= 1e-3.)
     float t0x, t0y, t0z, dtx, dty, dtz, kmx, kmy, kmz;
-    auto axis = [&](float dd, float inv, float oo, int c, int ax, float &t0, float &dt, float &kmax) {
-      const bool pos = dd >= 0.0f;
+    // The step direction comes from the culling inverse, not from d: safe_inv
+    // gives -0.0 the inverse -1e20, so `d >= 0` (true for -0.0) would pick the
+    // far face on the wrong side and step into cells the ray never enters.
+    auto axis = [&](float inv, float oo, int c, int ax, float &t0, float &dt, float &kmax) {
+      const bool pos = inv >= 0.0f;
       t0 = __builtin_fmaf(__builtin_fmaf(float(c + (pos ? 1 : 0)), G.h[ax], G.g0[ax]), inv, oo);
       dt = __builtin_fabsf(G.h[ax] * inv);
       kmax = float(pos ? G.n[ax] - 1 - c : c);
     };
-    axis(d.x, ix, ox, cx, 0, t0x, dtx, kmx);
+    axis(ix, ox, cx, 0, t0x, dtx, kmx);
     if constexpr (FLAT_Y) {  // the one layer's far y face (axis() at c = 0, no steps)
-      t0y = __builtin_fmaf(__builtin_fmaf(d.y >= 0.0f ? 1.0f : 0.0f, G.h[1], G.g0[1]), iy, oy);
+      t0y = __builtin_fmaf(__builtin_fmaf(iy >= 0.0f ? 1.0f : 0.0f, G.h[1], G.g0[1]), iy, oy);
       dty = kmy = 0.0f;
     } else {
-      axis(d.y, iy, oy, cy, 1, t0y, dty, kmy);
+      axis(iy, oy, cy, 1, t0y, dty, kmy);
     }
-    axis(d.z, iz, oz, cz, 2, t0z, dtz, kmz);
+    axis(iz, oz, cz, 2, t0z, dtz, kmz);
     float kx = 0.0f, ky = 0.0f, kz = 0.0f, tnx = t0x, tny = t0y, tnz = t0z;
     // the LDS address of the current cell's start, stepped by 4 x the cell step
     uint32_t cell = cells + 4u * uint32_t(cx + G.n[0] * (cy + G.n[1] * cz));
-    const int dcx = d.x >= 0.0f ? 4 : -4, dcy = d.y >= 0.0f ? 4 * G.n[0] : -4 * G.n[0];
-    const int dcz = d.z >= 0.0f ? 4 * G.n[0] * G.n[1] : -4 * G.n[0] * G.n[1];
+    const int dcx = ix >= 0.0f ? 4 : -4, dcy = iy >= 0.0f ? 4 * G.n[0] : -4 * G.n[0];
+    const int dcz = iz >= 0.0f ? 4 * G.n[0] * G.n[1] : -4 * G.n[0] * G.n[1];
 #if RTMI_TRACE_PHASES
     tp2 = __builtin_amdgcn_s_memtime();
 #endif

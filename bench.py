@@ -106,7 +106,7 @@ def launch(args, argv):
     visible, then run N ranks as a torch.distributed.run child and exit with
     its status.  This process never touches the GPU (no exec after GPU init)."""
     backend = os.environ.get("RTMI_DIST_BACKEND", "nccl")
-    n = visible_gpus()
+    n = 0 if STUB else visible_gpus()
     if backend == "nccl" and n < args.gpus:
         print(f"bench: {args.gpus} GPUs asked, {n} visible — refusing to report a {n}-GPU run as {args.gpus}",
               file=sys.stderr, flush=True)
@@ -126,6 +126,13 @@ def dist_setup(torch, dist):
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("RTMI_DIST_BACKEND", "nccl")
+    if STUB:  # CPU rehearsal: no device at all
+        if backend != "gloo":
+            raise SystemExit("bench: RTMI_BENCH_STUB=1 needs RTMI_DIST_BACKEND=gloo")
+        if world_size > 1:
+            dist.init_process_group("gloo")
+        cpu = torch.device("cpu")
+        return world_size, rank, -1, cpu, cpu
     ndev = torch.cuda.device_count()
     if backend == "nccl" and local_rank >= ndev:
         raise SystemExit(f"bench: rank {rank} needs GPU {local_rank}, {ndev} visible")
@@ -139,6 +146,53 @@ def dist_setup(torch, dist):
             dist.init_process_group("nccl", device_id=dev)
     coll = dev if backend == "nccl" else torch.device("cpu")
     return world_size, rank, device, dev, coll
+
+
+# ------------------------------------------------- CPU rehearsal (stub) ----
+# RTMI_BENCH_STUB=1 (with RTMI_DIST_BACKEND=gloo): the whole launch / rank
+# setup / timed loop / gather / gather-check / line assembly path on the CPU,
+# with a stand-in renderer that writes each pixel's image coordinates.  Used
+# by tests/test_bench_dist.py to rehearse N > 1 where no GPU exists; the line
+# it prints is marked "stub" and is never a measurement.
+STUB = os.environ.get("RTMI_BENCH_STUB") == "1"
+
+
+class StubRenderer:
+    """Stand-in for rt.Renderer (CPU): pixel (i, j) channel c of the strip =
+    (j * W + i) * 3 + c, so the value depends only on the image coordinates
+    (partition-invariant, like the product's RNG keys)."""
+
+    def __init__(self):
+        self._segs = 0
+
+    def render_rows(self, cam, W_, H_, S, D, seed, row0, row_step, nrows, buf):
+        import torch
+
+        j = row0 + row_step * np.arange(nrows)
+        v = (j[:, None] * W_ + np.arange(W_)[None, :])[:, :, None] * 3 + np.arange(3)[None, None, :]
+        buf.copy_(torch.from_numpy(np.where((j < H_)[:, None, None], v, 0).astype(np.float32)))
+        self._segs = int((j < H_).sum()) * W_ * S
+
+    def last_segments(self):
+        return self._segs
+
+    def __getattr__(self, name):  # set_schedule / set_kernel / set_accel / set_ordering / close
+        if name.startswith("set_") or name == "close":
+            return lambda *a, **k: None
+        raise AttributeError(name)
+
+
+class StubEvent:
+    """torch.cuda.Event stand-in (host clock)."""
+
+    def __init__(self, **_):
+        self.t = None
+
+    def record(self, stream=None):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, other):
+        return (other.t - self.t) * 1e3
 
 
 # ------------------------------------------------------- executed work ----
@@ -311,12 +365,27 @@ def cpu_baseline():
                                              "seconds": round(r["seconds"], 2)}
     except Exception as e:
         rows["iii_restatement_O3_native"] = {"error": str(e)[:200]}
+    # the share of one socket these rows use (north_star: "single-socket CPU
+    # reference"): row (ii) is bound by the reference's global rand() lock
+    # (128 threads on a full socket measured 0.052 Msamples/s,
+    # DESIGN.md §5), row (iii) scales with cores
+    cps = facts.get("cores_per_socket")
+    if isinstance(cps, int) and cps > 0:
+        facts["socket_share"] = round(threads / cps, 4)
+        r3 = rows.get("iii_restatement_O3_native", {})
+        if "value" in r3 and threads < cps:
+            r3["full_socket_linear_estimate"] = round(r3["value"] * cps / threads, 3)
+            r3["note"] = (f"{threads} of {cps} cores of one socket: a full socket would give up to ~{cps / threads:.0f}x "
+                          "this (linear estimate, not measured: the pool's CPU share per GPU job is "
+                          f"{threads} threads)")
     main_row = rows["ii_reference_O2"]
     if "value" not in main_row:
         return {"value": None, "unit": "Msamples/s", "cores": threads, "kind": "reference", "host": facts, "rows": rows}
     return {"value": main_row["value"], "unit": "Msamples/s", "cores": threads, "kind": "reference",
-            "sample": f"reference worker() g++ -O2 (oracle/_ref/ref_harness), {threads} std::threads pinned to one "
-                      f"socket, final scene {main_row['sample']} ({main_row['seconds']} s wall)",
+            "sample": f"reference worker() g++ -O2 (oracle/_ref/ref_harness), {threads} std::threads pinned to "
+                      f"{threads} physical cores of one socket (of {cps if cps else '?'}; the job's CPU share), final "
+                      f"scene {main_row['sample']} ({main_row['seconds']} s wall); bound by the reference's global "
+                      "rand() lock, so more cores do not raise it",
             "host": facts, "rows": rows}
 
 
@@ -417,7 +486,7 @@ def main():
 
     world = rt.random_scene()
     cam = rt.final_camera(W / H)
-    r = rt.Renderer(world, local_rank, tile_w=args.tile_w, chunk=args.chunk)
+    r = StubRenderer() if STUB else rt.Renderer(world, local_rank, tile_w=args.tile_w, chunk=args.chunk)
     r.set_schedule(args.chunk, args.tail_spp, args.tail_chunk)
     r.set_kernel(args.kernel)
     r.set_accel(args.accel)
@@ -425,20 +494,36 @@ def main():
     row0, row_step, nrows = rdist.strip_rows(H, rank, N)  # interleaved rows, row j -> rank j % N
     if args.strip_of > 1 and N == 1:  # analysis mode: one rank's share of an N-GPU render
         row0, row_step, nrows = rdist.strip_rows(H, 0, args.strip_of)
+    nrows_valid = len(range(row0, H, row_step))  # rows of this strip inside the image
     strip = torch.empty((nrows, W, 3), dtype=torch.float32, device=dev)
     tw = args.tile_w or rt.auto_tile_w(W, -(-(H - row0) // row_step) if row0 < H else 0)  # reported tile shape
     gathered = None
-    # a non-default stream: the kernel, its HIP events and the RCCL gather
-    # are all ordered on it (the null stream would bypass the events)
-    stream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(stream)
+    if STUB:
+        stream, Event = None, StubEvent
+
+        def sync():
+            pass
+
+        def render_into(rows, buf):
+            r.render_rows(cam, W, H, SPP, DEPTH, SEED, *rows, buf)
+    else:
+        # a non-default stream: the kernel, its HIP events and the RCCL gather
+        # are all ordered on it (the null stream would bypass the events)
+        stream, Event = torch.cuda.Stream(dev), torch.cuda.Event
+        torch.cuda.set_stream(stream)
+
+        def sync():
+            torch.cuda.synchronize(dev)
+
+        def render_into(rows, buf):
+            r.render_rows(cam, W, H, SPP, DEPTH, SEED, *rows, buf.data_ptr(), stream.cuda_stream)
 
     ev, gev = [], []
 
     def timed_render(rows=(row0, row_step, nrows), buf=strip):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0, e1 = Event(enable_timing=True), Event(enable_timing=True)
         e0.record(stream)
-        r.render_rows(cam, W, H, SPP, DEPTH, SEED, *rows, buf.data_ptr(), stream.cuda_stream)
+        render_into(rows, buf)
         e1.record(stream)
         return e0, e1
 
@@ -447,30 +532,30 @@ def main():
         if record:
             ev.append(timed_render())
         else:
-            r.render_rows(cam, W, H, SPP, DEPTH, SEED, row0, row_step, nrows, strip.data_ptr(), stream.cuda_stream)
+            render_into((row0, row_step, nrows), strip)
         if N > 1:  # the single exchange step: strips -> rank 0 over RCCL/xGMI
             if record:  # HIP events around the gather on the render's stream (it waits for the slowest rank)
-                g0 = torch.cuda.Event(enable_timing=True)
+                g0 = Event(enable_timing=True)
                 g0.record(stream)
-            gathered = rdist.gather_strips(strip if coll.type == "cuda" else strip.cpu(), rank, N, dst=0)
+            gathered = rdist.gather_strips(strip if coll.type == dev.type else strip.cpu(), rank, N, dst=0)
             if record:
-                g1 = torch.cuda.Event(enable_timing=True)
+                g1 = Event(enable_timing=True)
                 g1.record(stream)
                 gev.append((g0, g1))
 
     for _ in range(args.warmup):
         step(False)
-    torch.cuda.synchronize(dev)
+    sync()
     if N > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
-    torch.cuda.synchronize(dev)
+    sync()
     if N > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     elapsed = my_elapsed = time.perf_counter() - t0
     if N > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
@@ -509,7 +594,7 @@ def main():
         if rank == 0:
             full = torch.empty((H, W, 3), dtype=torch.float32, device=dev)
             e0, e1 = timed_render((0, 1, H), full)
-            torch.cuda.synchronize(dev)
+            sync()
             img = rdist.unpermute([g.cpu().numpy() for g in gathered], H)
             ref = full.cpu().numpy()
             equal = bool(np.array_equal(img, ref))
@@ -528,8 +613,10 @@ def main():
         e0, e1 = timed_render()
         r.set_ordering("none")
         e2, e3 = timed_render()
-        torch.cuda.synchronize(dev)
+        sync()
         one_shot = {"probe_ordered_ms": round(e0.elapsed_time(e1), 3), "image_order_ms": round(e2.elapsed_time(e3), 3)}
+        if N == 1:  # this rank's rows are the whole workload (or the --strip-of strip)
+            one_shot["msamples_per_s"] = round(nrows_valid * W * SPP / (one_shot["probe_ordered_ms"] * 1e-3) / 1e6, 3)
         r.set_ordering(args.ordering)
 
     # The brute-force kernel's own VALU roofline: one more launch of the same
@@ -538,7 +625,7 @@ def main():
     if args.accel != "none" and rank == 0 and not args.timed_only:
         r.set_accel("none")
         e0, e1 = timed_render()
-        torch.cuda.synchronize(dev)
+        sync()
         bf_ms = e0.elapsed_time(e1)
         bf_segs = r.last_segments()
         r.set_accel(args.accel)
@@ -552,8 +639,8 @@ def main():
         counts, why = None, None
         if args.accel == "none":
             flop_exec = flop_eq  # brute force executes every miss test
-        elif args.no_exec_counts:
-            flop_exec, why = None, "skipped (--no-exec-counts)"
+        elif args.no_exec_counts or STUB:
+            flop_exec, why = None, "skipped (stub renderer)" if STUB else "skipped (--no-exec-counts)"
         else:
             counts, why = executed_counts(W, H, SPP, row0, row_step, nrows, args.accel)
             flop_exec = executed_flop(counts, args.accel) if counts else None
@@ -633,6 +720,11 @@ def main():
         line = {
             "metric": METRIC,
             "value": round(value, 3),
+            # the reference's use case renders once (main.cpp:292-360): a render
+            # with no cost map of its layout runs a 1-2 spp probe pass first
+            # (kernel time of that one render, HIP events); the timed steps
+            # above reuse the previous identical render's map (config.timed_steps)
+            "one_shot_msamples_per_s": (one_shot or {}).get("msamples_per_s"),
             "unit": "Msamples/s",
             "n_gpus": N,
             "steps": args.steps,
@@ -642,7 +734,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": round(value / PUBLISHED_CPU_MSPS, 1),
             "dtype": "f32",
-            "data": "synthetic: RTIOW final scene regenerated from glibc rand() seed 1 (487 spheres, = reference)",
+            "data": ("STUB renderer: CPU rehearsal of the launch / rank / gather / line path, not a measurement"
+                     if STUB else "synthetic: RTIOW final scene regenerated from glibc rand() seed 1 (487 spheres, = reference)"),
             "config": {
                 "workload": f"rtiow_final_{W}x{H}_{SPP}spp_depth{DEPTH}",
                 "width": W, "height": H, "spp": SPP, "max_depth": DEPTH, "seed": SEED, "spheres": len(world),
@@ -651,11 +744,17 @@ def main():
                 "kernel": args.kernel,
                 "accel": args.accel,
                 "ordering": args.ordering,
+                "timed_steps": ("each step re-renders the same workload; with ordering 'cost' it dispatches tiles by the "
+                                "previous identical render's per-tile cost map (RT_ORDER_COST): the first render of a "
+                                "layout (warmup) pays a 1-2 spp probe pass instead, see one_shot_msamples_per_s"
+                                if args.ordering == "cost" else "image-order dispatch, no cost map"),
             },
             "roofline": roof,
             "one_shot": one_shot,
             "vs_baseline_ref": "published CPU rt_in_one_weekend 0.1189 Msamples/s (README.md:16-19)",
         }
+        if STUB:
+            line["stub"] = True
         if dist_info is not None:
             line["dist"] = dist_info
         if gather_check is not None:

@@ -470,4 +470,47 @@ int32_t or_fast_sample(const or_scene *s, const or_camera *c, int32_t W, int32_t
   free(w.s);
   return (int32_t)segs;
 }
+/* The fast mode's image-plane coordinate (i + r) * (1/D) (fast_sample
+ * above; the kernels' camera_ray reads the same reciprocal) against the
+ * quotient (i + r) / D of main.cpp:278-279 in float, D = W-1 or H-1, over
+ * EVERY numerator the fast path can form: column (row) i in [0, D], jitter
+ * r = k 2^-24, k in [0, 2^24) (xo_pair's 24-bit uniforms).  fl(i + r) takes
+ * exactly the values k 2^-24 (i = 0) and every float in [1, D + 1] (i >= 1:
+ * the float spacing in [i, i+1) is a multiple of 2^-24, and a sum rounded up
+ * gives i + 1), so those sets are enumerated instead of the D 2^24 pairs.
+ * Returns the largest distance between the two results in ulps; counts the
+ * numerators checked and those whose two results differ. */
+int32_t or_uv_forms(int32_t D, int64_t *n_checked, int64_t *n_diff) {
+  const float d = (float)D, inv = 1.0f / d;
+  uint32_t hi_bits;
+  {
+    const float top = (float)D + 1.0f;
+    memcpy(&hi_bits, &top, 4);
+  }
+  const uint32_t one_bits = 0x3F800000u;
+  const int64_t n_low = (int64_t)1 << 24, n_high = (int64_t)(hi_bits - one_bits) + 1;
+  int32_t worst = 0;
+  int64_t diff = 0;
+#pragma omp parallel for schedule(static) reduction(max : worst) reduction(+ : diff)
+  for (int64_t q = 0; q < n_low + n_high; q++) {
+    float x;
+    if (q < n_low) {
+      x = (float)q * 0x1p-24f;  /* i = 0 */
+    } else {
+      const uint32_t b = one_bits + (uint32_t)(q - n_low);
+      memcpy(&x, &b, 4);
+    }
+    const float prod = x * inv, quot = x / d;
+    int32_t pb, qb;
+    memcpy(&pb, &prod, 4);
+    memcpy(&qb, &quot, 4);
+    const int32_t dist = pb > qb ? pb - qb : qb - pb;  /* both >= +0: bit distance = ulps */
+    if (dist > worst) worst = dist;
+    diff += dist != 0;
+  }
+  if (n_checked) *n_checked = n_low + n_high;
+  if (n_diff) *n_diff = diff;
+  return worst;
+}
+
 #include "rt_nw_oracle.inc"

@@ -200,6 +200,51 @@ def test_multi_renderer_reuses_contexts_passes_and_times(final_world, final_rend
         m.close()
 
 
+def test_multi_create_fails_cleanly_after_partial_setup(final_world, final_renderer):
+    """rt_multi_create with a scene that the device context rejects (an
+    unknown material kind: rt_ctx_set_scene fails after rt_ctx_create has
+    made device 0's context) returns the error with no handle and leaves
+    nothing behind: a good device set made next renders the same bits."""
+    bad = rt.World(final_world.center_radius.copy(), final_world.mat_kind.copy(), final_world.mat_params.copy())
+    bad.mat_kind[7] = 9
+    L = rt.load()
+    h = C.c_void_p()
+    sc = bad.c_struct()
+    rc = L.rt_multi_create(C.byref(sc), 1, C.byref(h))
+    assert rc == -4 and not h.value  # RT_EUNSUPPORTED
+    assert b"material kind" in L.rt_last_error()
+    W, H, S = 24, 16, 3
+    cam = rt.final_camera(W / H)
+    m = rt.MultiRenderer(final_world, n_gpus=1)
+    try:
+        assert np.array_equal(m.render(cam, W, H, S, 50, SEED), final_renderer.render(cam, W, H, S, 50, SEED))
+    finally:
+        m.close()
+
+
+def test_multi_failed_pass_invalidates_the_accumulators(final_world, final_renderer):
+    """A progressive pass that fails on a device leaves the device set's
+    accumulators covering different sample ranges: rt_multi_accum_resolve
+    refuses them until rt_multi_accum_reset, and a reset set
+    resolves to the one-render bits again."""
+    W, H = 24, 16
+    cam = rt.final_camera(W / H)
+    m = rt.MultiRenderer(final_world, n_gpus=1)
+    try:
+        m.accum_reset(W, H)
+        m.render_pass(cam, 0, 2)
+        with pytest.raises(RuntimeError):
+            m.render_pass(cam, 2, 2, max_depth=-1)  # rejected on device 0
+        with pytest.raises(RuntimeError):
+            m.accum_resolve()
+        m.accum_reset(W, H)
+        m.render_pass(cam, 0, 2)
+        m.render_pass(cam, 2, 2)
+        assert np.array_equal(m.accum_resolve(), final_renderer.render(cam, W, H, 4, 50, SEED))
+    finally:
+        m.close()
+
+
 # ---------------------------------------------------- full-size properties -
 @pytest.fixture(scope="module")
 def config2(final_renderer):
@@ -398,8 +443,8 @@ def test_bvh_config2_equals_brute_force(accel, config2, final_renderer):
 @pytest.mark.parametrize("accel", ["bvh", "grid"])
 def test_bvh_adversarial_rays_equal_brute_force(accel, final_world):
     """1M random rays: origins in the field and just off sphere surfaces
-    (both sides), directions with exactly-zero components and along cell
-    planes; the BVH's / grid's closest hit (index and t) equals the
+    (both sides), directions with exactly-zero components (+0.0 and -0.0)
+    and along cell planes; the BVH's / grid's closest hit (index and t) equals the
     brute-force loop's for every ray (rt_ctx_debug_hits, a validation entry
     point)."""
     r = rt.Renderer(final_world, 0)
@@ -415,12 +460,13 @@ def test_bvh_adversarial_rays_equal_brute_force(accel, final_world):
     u /= np.linalg.norm(u, axis=1, keepdims=True)
     o[: n // 2] = c + u * (rad[:, None] * (1 + g.choice([1e-3, 1e-4, -1e-4, 1e-6, 0.0], n // 2)[:, None]))
     dv = g.normal(size=(n, 3)) * g.choice([0.3, 1.0, 3.0], n)[:, None]
-    dv[g.random((n, 3)) < 0.03] = 0.0
+    z = g.random((n, 3)) < 0.03
+    dv[z] = np.where(g.random(int(z.sum())) < 0.5, 0.0, -0.0)  # exact zeros of both signs
     # grazing rays inside the sphere layer (long DDA walks) and rays from
     # integer grid-like coordinates
     m = n // 8
     o[-m:, 1] = g.uniform(0.0, 0.45, m)
-    dv[-m:, 1] = g.choice([0.0, 1e-3, -1e-3, 0.05], m)
+    dv[-m:, 1] = g.choice([0.0, -0.0, 1e-3, -1e-3, 0.05], m)
     o[-2 * m:-m, [0, 2]] = np.round(o[-2 * m:-m, [0, 2]] * 2) / 2
     dv[np.all(dv == 0, axis=1)] = [0, -1, 0]  # no zero directions (not a ray)
     rays = np.ascontiguousarray(np.column_stack([o, dv]).astype(np.float32))
@@ -484,7 +530,8 @@ def test_grid_general_and_one_layer_walks(final_world):
         u /= np.linalg.norm(u, axis=1, keepdims=True)
         o[: m // 2] = cr[k, :3] + u * (cr[k, 3:4] * (1 + g.choice([1e-3, 1e-4, -1e-4, 0.0], m // 2)[:, None]))
         dv = g.normal(size=(m, 3))
-        dv[g.random((m, 3)) < 0.03] = 0.0
+        z = g.random((m, 3)) < 0.03
+        dv[z] = np.where(g.random(int(z.sum())) < 0.5, 0.0, -0.0)  # exact zeros of both signs
         dv[np.all(dv == 0, axis=1)] = [0, -1, 0]
         rays = np.ascontiguousarray(np.column_stack([o, dv]).astype(np.float32))
         idx = np.zeros(2 * m, np.int32)

@@ -317,3 +317,44 @@ def test_spheres_only_moving_and_not_simple_scenes():
         k = r.last_kernel()
         r.close()
         assert k["spheres_only"] == 0, (extra, k)
+
+
+_TRACE_CHILD = r"""
+import os, sys
+import numpy as np
+sys.path.insert(0, os.environ["RTMI_REPO"])
+import a_dive_into_ray_tracing_amd.nextweek as nw
+img = nw.load_image(os.path.join(os.environ["RTMI_REPO"], "tests", "golden", "earthmap.jpeg"))
+out = {}
+for which in (1, 8):
+    s, cam = nw.preset(which, image=img, aspect=1.0)
+    r = nw.NwRenderer(s)
+    for (i, j) in ((3, 5), (12, 9)):
+        f, k = r.debug_trace(cam, 16, 16, i, j, 2)
+        out[f"f{which}_{i}_{j}"], out[f"k{which}_{i}_{j}"] = f, k
+    r.close()
+np.savez(sys.argv[1], **out)
+"""
+
+
+@pytest.mark.parametrize("lib", ["librtmi_stats.so"])
+def test_debug_trace_on_the_stats_build(lib, tmp_path):
+    """rt_nw_debug_trace runs on the RTMI_STATS build too (its trace kernel
+    hands the walk a counter of its own: ADVICE r03 found a null counter
+    pointer there), and records the same segments as the product library."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for name in ("librtmi.so", lib):
+        env = dict(os.environ, RTMI_REPO=root, RTMI_LIBRARY=os.path.join(root, "a_dive_into_ray_tracing_amd", "lib", name))
+        p = subprocess.run([sys.executable, "-c", _TRACE_CHILD, str(tmp_path / name)], env=env, capture_output=True,
+                           text=True, timeout=240)
+        assert p.returncode == 0, p.stderr[-2000:]
+        res[name] = np.load(str(tmp_path / name) + ".npz")
+    a, b = res["librtmi.so"], res[lib]
+    assert sorted(a.files) == sorted(b.files)
+    for key in a.files:
+        assert a[key].shape[0] >= 1
+        assert np.array_equal(a[key], b[key]), key

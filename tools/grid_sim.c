@@ -109,6 +109,19 @@ static void build(double density) {
 }
 
 /* one segment's walk: the list lengths of the cells visited (returns their count) */
+static int g_pred;  /* the walk's cell-count bound known before it: |dcx|+|dcy|+|dcz|+1 (0: no walk) */
+static int g_pred_nobig;  /* the same bound from the grid box alone (before the big-sphere pass) */
+static int bound_of(const Ray *r, const double inv[3], double tmax) {
+  double tn = 0, tf = tmax;
+  for (int k = 0; k < 3; k++) { double t0 = (g0[k]-r->o[k])*inv[k], t1 = (g0[k]+n[k]*h[k]-r->o[k])*inv[k];
+    if (t0 > t1) { double x = t0; t0 = t1; t1 = x; } if (t0 > tn) tn = t0; if (t1 < tf) tf = t1; }
+  if (tn > tf) return 0;
+  int b = 1;
+  for (int k = 0; k < 3; k++) { double p0 = r->o[k] + tn*r->d[k], p1 = r->o[k] + tf*r->d[k];
+    int c0 = (int)floor((p0-g0[k])/h[k]), c1 = (int)floor((p1-g0[k])/h[k]);
+    if (c0 < 0) c0 = 0; if (c0 >= n[k]) c0 = n[k]-1; if (c1 < 0) c1 = 0; if (c1 >= n[k]) c1 = n[k]-1; b += abs(c1 - c0); }
+  return b;
+}
 static int walk(const Ray *r, int *lens, int *entry_cell) {
   double a = r->d[0]*r->d[0]+r->d[1]*r->d[1]+r->d[2]*r->d[2], tmax = INFINITY;
   for (int i = 0; i < nbig; i++) { int q = big_[i];
@@ -120,10 +133,12 @@ static int walk(const Ray *r, int *lens, int *entry_cell) {
     if (rt < 0.001 || rt > tmax) { rt = (-hb+sq)/a; if (rt < 0.001 || rt > tmax) continue; }
     tmax = rt; }
   double inv[3], tn = 0, tf = tmax;
-  for (int k = 0; k < 3; k++) { inv[k] = 1.0 / (fabs(r->d[k]) < 1e-20 ? copysign(1e-20, r->d[k]) : r->d[k]);
+  for (int k = 0; k < 3; k++) inv[k] = 1.0 / (fabs(r->d[k]) < 1e-20 ? copysign(1e-20, r->d[k]) : r->d[k]);
+  g_pred_nobig = bound_of(r, inv, INFINITY);
+  for (int k = 0; k < 3; k++) {
     double t0 = (g0[k]-r->o[k])*inv[k], t1 = (g0[k]+n[k]*h[k]-r->o[k])*inv[k];
     if (t0 > t1) { double x = t0; t0 = t1; t1 = x; } if (t0 > tn) tn = t0; if (t1 < tf) tf = t1; }
-  *entry_cell = -1;
+  *entry_cell = -1; g_pred = 0;
   if (tn > tf) return 0;
   int c[3], step[3]; double tnext[3], dt[3];
   for (int k = 0; k < 3; k++) { double p = r->o[k] + tn*r->d[k]; c[k] = (int)floor((p-g0[k])/h[k]);
@@ -131,6 +146,9 @@ static int walk(const Ray *r, int *lens, int *entry_cell) {
     step[k] = r->d[k] >= 0 ? 1 : -1; dt[k] = fabs(h[k]*inv[k]);
     tnext[k] = (g0[k] + (c[k] + (step[k] > 0)) * h[k] - r->o[k]) * inv[k]; }
   *entry_cell = c[0] + n[0]*(c[1] + n[1]*c[2]);
+  g_pred = 1;
+  for (int k = 0; k < 3; k++) { double p = r->o[k] + tf*r->d[k]; int e = (int)floor((p-g0[k])/h[k]);
+    if (e < 0) e = 0; if (e >= n[k]) e = n[k]-1; g_pred += abs(e - c[k]); }
   int nc = 0;
   for (;;) {
     int cell = c[0] + n[0]*(c[1] + n[1]*c[2]);
@@ -155,7 +173,7 @@ static int walk(const Ray *r, int *lens, int *entry_cell) {
   return nc;
 }
 
-typedef struct { int nc, oct, cell, lens[128]; unsigned long long cand[128], use[128]; } Walk;
+typedef struct { int nc, oct, cell, pred, pnb, lens[128]; unsigned long long cand[128], use[128]; } Walk;
 static Walk *W;
 static int key_mode;
 static int key_of(const Walk *w) {
@@ -163,7 +181,10 @@ static int key_of(const Walk *w) {
     case 0: return w->oct;
     case 1: return w->cell;
     case 2: return w->oct * 100000 + w->cell + 1;
-    default: return w->nc;
+    case 3: return w->nc;
+    case 4: return w->pred;
+    case 5: return w->pred > 15 ? 15 : w->pred;
+    default: return w->pnb;
   }
 }
 static int cmpk(const void *x, const void *y) {
@@ -311,6 +332,7 @@ int main(int argc, char **argv) {
   for (int i = 0; i < nseg; i++) {
     g_cand = W[i].cand; g_use = W[i].use;
     W[i].nc = walk(&segs[i], W[i].lens, &W[i].cell);
+    W[i].pred = g_pred; W[i].pnb = g_pred_nobig;
     W[i].oct = (segs[i].d[0] < 0) | ((segs[i].d[1] < 0) << 1) | ((segs[i].d[2] < 0) << 2);
   }
   int *ids = malloc(nseg * sizeof(int));
@@ -362,9 +384,19 @@ int main(int argc, char **argv) {
     for (int thr = 1; thr <= 32; thr *= 2) printf("  thr %d: %.3f", thr, early_exit(thr) / base);
     printf("\n");
   }
-  const char *kn[4] = {"oct", "cell", "oct+cell", "len"};
+  { /* how well the bound predicts the walk's length */
+    double sp = 0, sn = 0, spn = 0, spp = 0, snn = 0, ex = 0; long hist[17] = {0};
+    for (int i = 0; i < nseg; i++) { double x = W[i].pred, y = W[i].nc; sp += x; sn += y; spn += x*y; spp += x*x; snn += y*y;
+      ex += x == y; hist[W[i].pred > 16 ? 16 : W[i].pred]++; }
+    const double mp = sp/nseg, mn = sn/nseg;
+    printf("  bound vs walk: mean bound %.3f, mean cells %.3f, exact %.3f, corr %.3f; bound histogram:", mp, mn, ex/nseg,
+           (spn/nseg - mp*mn) / sqrt((spp/nseg - mp*mp) * (snn/nseg - mn*mn)));
+    for (int k = 0; k <= 16; k++) printf(" %.3f", (double)hist[k]/nseg);
+    printf("\n");
+  }
+  const char *kn[7] = {"oct", "cell", "oct+cell", "len", "bound", "bound15", "boxbound"};
   for (int block = 256; block <= 1024; block *= 2)
-    for (key_mode = 0; key_mode < 4; key_mode++) {
+    for (key_mode = 0; key_mode < 7; key_mode++) {
       Acc b = {0};
       for (int t = 0; t < ntiles; t++) for (int i = tile_start[t]; i < tile_start[t+1]; i += block) {
         int nb = tile_start[t+1] - i < block ? tile_start[t+1] - i : block;

@@ -125,6 +125,9 @@ __device__ unsigned g_trace_n;
 #ifndef RTMI_PERSIST_MIN_BLOCKS
 #define RTMI_PERSIST_MIN_BLOCKS 1
 #endif
+#ifndef RTMI_BLOCK_POOL
+#define RTMI_BLOCK_POOL 0
+#endif
 #ifndef RTMI_PAIR_GROUP
 #define RTMI_PAIR_GROUP 4
 #endif
@@ -354,25 +357,43 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   constexpr int WPB = GridShape<ACC != 0>::waves;
   __shared__ unsigned long long acc[WPB][3][64];
   __shared__ float cam_lds[21];  // the camera (stage_camera)
+  __shared__ int job_next;       // block-shared jobs: the next unclaimed one
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * WPB + wave;
+  if (threadIdx.x == 0) job_next = 0;  // (published by the staging barrier)
   stage_camera(cam_lds, a);
   if constexpr (ACC == 0) __syncthreads();  // (accelerated kernels: stage_* ends with one)
   if constexpr (ACC == 1) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
   else if constexpr (ACC >= 2) stage_grid(a.acc);
   if (item >= a.n_items) return;  // wave-uniform; no block barrier follows
 
+  auto item_range = [&](int it, int &tl, int &sb, int &n) {
+    if (it < a.tiles * a.nch1) {
+      tl = it / a.nch1;
+      sb = (it - tl * a.nch1) * a.chunk1;
+      n = max(0, min(a.chunk1, a.spp1 - sb));  // 0: an empty item of the automatic schedule
+    } else {
+      const int i2 = it - a.tiles * a.nch1;
+      tl = i2 / a.nch2;
+      sb = a.spp1 + (i2 - tl * a.nch2) * a.chunk2;
+      n = max(0, min(a.chunk2, a.spp - sb));
+    }
+  };
   int tile, s0, ns;
-  if (item < a.tiles * a.nch1) {
-    tile = item / a.nch1;
-    s0 = (item - tile * a.nch1) * a.chunk1;
-    ns = max(0, min(a.chunk1, a.spp1 - s0));  // 0: an empty item of the automatic schedule
-  } else {
-    const int i2 = item - a.tiles * a.nch1;
-    tile = i2 / a.nch2;
-    s0 = a.spp1 + (i2 - tile * a.nch2) * a.chunk2;
-    ns = max(0, min(a.chunk2, a.spp - s0));
+  item_range(item, tile, s0, ns);
+  // Block-shared jobs (RTMI_BLOCK_POOL; block_flush launches, whose block
+  // items are consecutive sample ranges of one tile): the block's waves take
+  // 64-job batches of their items' union from one LDS counter, so no wave runs
+  // out of jobs while its block has some, and the waves ramp down together.
+  // Jobs map to (pixel, sample) as before: the same rays, the same image.
+  const bool shared_jobs = CHUNKED && RTMI_BLOCK_POOL && a.block_flush;
+  if (shared_jobs) {
+    int t_, s_, n_, t2_, s2_, n2_;
+    item_range(blockIdx.x * WPB, t_, s_, n_);
+    item_range(min(blockIdx.x * WPB + WPB, a.n_items) - 1, t2_, s2_, n2_);
+    s0 = s_;
+    ns = s2_ + n2_ - s_;
   }
   if (a.tile_order) tile = a.tile_order[tile];  // expensive tiles first
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
@@ -443,9 +464,16 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   // for the few lanes that regenerate.  Same rays bit for bit.
   V3<float> po, pd;
   Xoro prng;
-  int pbase = 0, ppos = 64;  // wave-uniform: job of slot 0, next unused slot
-  camera_ray(lane, po, pd, prng);
-  adopt(lane, po, pd, prng);
+  // the next 64 jobs of this wave (wave-private) or of the block (shared)
+  auto claim = [&](int prev) {
+    if (!shared_jobs) return prev + 64;
+    int v = 0;
+    if (lane == 0) v = atomicAdd(&job_next, 64);
+    return __builtin_amdgcn_readfirstlane(v);
+  };
+  int pbase = __builtin_amdgcn_readfirstlane(claim(-64)), ppos = 64;  // wave-uniform: job of slot 0, next unused slot
+  if (pbase < nq) camera_ray(pbase + lane, po, pd, prng);
+  adopt(pbase + lane, po, pd, prng);
   auto pull = [](int src4, float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(src4, __float_as_int(v))); };
   auto pull64 = [](int src4, uint64_t v) {
     const uint32_t lo = uint32_t(__builtin_amdgcn_ds_bpermute(src4, int(uint32_t(v))));
@@ -485,7 +513,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
       const int cnt = __popcll(m);
       for (int served = 0; served < cnt;) {
         if (ppos == 64) {
-          pbase = __builtin_amdgcn_readfirstlane(pbase + 64);
+          pbase = __builtin_amdgcn_readfirstlane(claim(pbase));
           ppos = 0;
           if (pbase < nq) camera_ray(pbase + lane, po, pd, prng);
         }

@@ -274,6 +274,68 @@ static void report(const char *name, const Acc *a) {
          a->lane_cells / (64 * a->wave_cells), a->lane_spheres / (64 * a->wave_spheres));
 }
 
+/* Instruction-cost model of the walk (round 4), from the ISA of
+ * render_kernel<8, true, 3> (make -C a_dive_into_ray_tracing_amd/csrc asm):
+ * a cell iteration ~30 instructions (range read, the select step, loop
+ * masks), a sphere iteration ~14 (reference + record reads, 8 FMAs, compare,
+ * mask) and a root resolution ~33 more whenever any lane of the wave has a
+ * candidate there.  A pass costs ~850 VALU wave-instructions in all (1.78e10
+ * per config-2 launch over ~2.1e7 wave-passes), so ~400 outside the walk. */
+static double CI_CELL = 30, CI_SPH = 14, CI_RES = 33, CI_REST = 400;
+static double walk_instr(const int *ids, int nl, double *wave_time) {
+  int maxc = 0;
+  for (int l = 0; l < nl; l++) if (W[ids[l]].nc > maxc) maxc = W[ids[l]].nc;
+  double c = 0;
+  for (int s = 0; s < maxc; s++) {
+    int m = 0;
+    for (int l = 0; l < nl; l++) { const Walk *w = &W[ids[l]]; if (s < w->nc && w->lens[s] > m) m = w->lens[s]; }
+    c += CI_CELL + m * CI_SPH;
+    for (int k = 0; k < m; k++) {
+      int any = 0;
+      for (int l = 0; l < nl && !any; l++) { const Walk *w = &W[ids[l]]; if (s < w->nc && k < w->lens[s] && ((w->cand[s] >> k) & 1)) any = 1; }
+      c += any ? CI_RES : 0;
+    }
+  }
+  if (wave_time) *wave_time = c;
+  return c;
+}
+
+/* Regrouping a block's rays by the walk-length bound before the walk
+ * (VERDICT r03 item 1), charged honestly: per wave-pass the rest of the pass
+ * (CI_REST), the walk of the rays the wave holds after the sort, and the
+ * exchange E (key from the exit cell, per-bin ballots and the block prefix,
+ * the ray state through LDS and back, three barriers).  Rays with bound 0
+ * (no walk) are not exchanged.  Also the barrier idle time: in a block pass
+ * every wave waits at the walk's closing barrier for the block's longest walk
+ * (sum over waves of max - own), which only other blocks' waves can fill. */
+static void regroup_cost(int block, double E) {
+  double base = 0, regroup = 0, idle = 0, passes = 0, wbase = 0, wreg = 0;
+  int *ids = malloc(block * sizeof(int)), *walkers = malloc(block * sizeof(int));
+  for (int t = 0; t < ntiles; t++)
+    for (int i = tile_start[t]; i + block <= tile_start[t + 1]; i += block) {
+      for (int w = 0; w < block; w += 64) {  /* today: each wave its own 64 rays */
+        for (int l = 0; l < 64; l++) ids[l] = i + w + l;
+        const double c = walk_instr(ids, 64, NULL);
+        base += CI_REST + c; wbase += c; passes += 1;
+      }
+      int nw = 0;
+      for (int l = 0; l < block; l++) if (W[i + l].pred > 0) walkers[nw++] = i + l;
+      key_mode = 4;
+      qsort(walkers, nw, sizeof(int), cmpk);
+      double mx = 0, sum = 0;
+      for (int w = 0; w < block; w += 64) {
+        double c = 0;
+        if (w < nw) walk_instr(walkers + w, nw - w < 64 ? nw - w : 64, &c);
+        regroup += CI_REST + E + c; wreg += c; sum += c; if (c > mx) mx = c;
+      }
+      idle += (block / 64) * mx - sum;
+    }
+  printf("  regroup %4d rays, exchange %3.0f instr/wave-pass: walk %.1f -> %.1f instr/wave-pass (%.3f), pass %.1f -> %.1f "
+         "(net %+.1f%%), barrier idle %.1f per wave-pass (%.1f%% of the new pass)\n", block, E, wbase / passes, wreg / passes,
+         wreg / wbase, base / passes, regroup / passes, 100 * (regroup / base - 1), idle / passes, 100 * idle / regroup);
+  free(ids); free(walkers);
+}
+
 int main(int argc, char **argv) {
   FILE *f = fopen(argc > 1 ? argv[1] : "tests/golden/scene_final.txt", "r");
   if (!f || fscanf(f, "%d", &N) != 1) return 1;
@@ -360,6 +422,28 @@ int main(int argc, char **argv) {
       it*64/nseg, anyc*64/nseg, anyu*64/nseg, lc/nseg, lu/nseg);
   }
 
+  /* Deferred root resolution (round 4): a lane keeps its first candidate of
+   * a cell (hb, disc, index) and resolves it after the cell's sphere loop; a
+   * second candidate in the same cell resolves the kept one in the loop
+   * first.  Wave-level resolution blocks per wave-segment: today one per
+   * sphere position where some lane has a candidate; deferred, one per
+   * position where some lane has its 2nd+ candidate of the cell, plus one
+   * per cell step where some lane kept one. */
+  { double now = 0, in_loop = 0, at_end = 0;
+    for (int i = 0; i < nseg; i += 64) { int nl = nseg - i < 64 ? nseg - i : 64; int maxc = 0;
+      for (int l = 0; l < nl; l++) if (W[i+l].nc > maxc) maxc = W[i+l].nc;
+      for (int c = 0; c < maxc; c++) {
+        int m = 0; for (int l = 0; l < nl; l++) if (c < W[i+l].nc && W[i+l].lens[c] > m) m = W[i+l].lens[c];
+        int seen[64] = {0}, kept = 0;
+        for (int k = 0; k < m; k++) { int any = 0, second = 0;
+          for (int l = 0; l < nl; l++) { const Walk *w = &W[i+l]; if (c < w->nc && k < w->lens[c] && ((w->cand[c] >> k) & 1)) {
+            any = 1; if (seen[l]) second = 1; seen[l] = 1; kept = 1; } }
+          now += any; in_loop += second; }
+        at_end += kept; } }
+    printf("  root resolutions per wave-seg: today %.3f, deferred %.3f (in the loop %.3f + after the cell %.3f)\n",
+           now * 64 / nseg, (in_loop + at_end) * 64 / nseg, in_loop * 64 / nseg, at_end * 64 / nseg);
+  }
+
   { Acc p = {0}, q = {0}, r = {0}; int np = 0;
     for (int i = 0; i < nseg; i += 64) { int nl = nseg - i < 64 ? nseg - i : 64; int ip[64], is[64], npp = 0, ns = 0;
       for (int l = 0; l < nl; l++) { if (segs[i+l].depth == 0) ip[npp++] = i + l; else is[ns++] = i + l; }
@@ -394,6 +478,9 @@ int main(int argc, char **argv) {
     for (int k = 0; k <= 16; k++) printf(" %.3f", (double)hist[k]/nseg);
     printf("\n");
   }
+  if (getenv("CI_REST")) CI_REST = atof(getenv("CI_REST"));
+  for (int block = 256; block <= 512; block *= 2)
+    for (double E = 0; E <= 120; E += 40) regroup_cost(block, E);
   const char *kn[7] = {"oct", "cell", "oct+cell", "len", "bound", "bound15", "boxbound"};
   for (int block = 256; block <= 1024; block *= 2)
     for (key_mode = 0; key_mode < 7; key_mode++) {

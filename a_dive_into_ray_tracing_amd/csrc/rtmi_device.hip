@@ -388,12 +388,15 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   // out of jobs while its block has some, and the waves ramp down together.
   // Jobs map to (pixel, sample) as before: the same rays, the same image.
   const bool shared_jobs = CHUNKED && RTMI_BLOCK_POOL && a.block_flush;
-  if (shared_jobs) {
-    int t_, s_, n_, t2_, s2_, n2_;
-    item_range(blockIdx.x * WPB, t_, s_, n_);
-    item_range(min(blockIdx.x * WPB + WPB, a.n_items) - 1, t2_, s2_, n2_);
-    s0 = s_;
-    ns = s2_ + n2_ - s_;
+  if (shared_jobs) {  // the union of the block's items: consecutive sample ranges (the last ones may be empty)
+    const int first = blockIdx.x * WPB, last = min(first + WPB, a.n_items);
+    int t_, n_;
+    item_range(first, t_, s0, ns);
+    for (int it = first + 1; it < last; ++it) {
+      int s_;
+      item_range(it, t_, s_, n_);
+      ns += n_;
+    }
   }
   if (a.tile_order) tile = a.tile_order[tile];  // expensive tiles first
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;

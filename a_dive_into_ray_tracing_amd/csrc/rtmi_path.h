@@ -517,7 +517,19 @@ __host__ __device__ constexpr size_t grid_lds_bytes(int32_t nsph, int32_t ncells
   return size_t(nsph) * 16 + (size_t(ncells) + 1) * 4 + size_t(nrefs) * 4;
 }
 
+#ifndef RTMI_GRID_LDS
+#define RTMI_GRID_LDS 0
+#endif
+#if RTMI_GRID_LDS
+// The grid descriptor in LDS (staged with the grid): the walk setup reads its
+// fields there instead of holding them in scalar registers, which overflow the
+// kernel's SGPR budget into VGPR lanes read back with v_readlane.
+__shared__ GridDesc rtmi_grid_desc;
+#endif
 __device__ __forceinline__ void stage_grid(const Accel &g) {
+#if RTMI_GRID_LDS
+  if (threadIdx.x == 0) rtmi_grid_desc = g.grid;
+#endif
   for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) rtmi_bvh_lds[i] = g.sph[i];
   uint32_t *c = reinterpret_cast<uint32_t *>(rtmi_bvh_lds + g.nsph);
   uint32_t *r = c + g.grid.ncells + 1;
@@ -547,6 +559,9 @@ __device__ __forceinline__ float safe_inv(float v) {
 
 #ifndef RTMI_TRACE_PHASES
 #define RTMI_TRACE_PHASES 0
+#endif
+#ifndef RTMI_DEFER_RESOLVE
+#define RTMI_DEFER_RESOLVE 0
 #endif
 
 
@@ -685,7 +700,11 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
   pc.c[0] += tp1 - tp0;
   unsigned long long tp2 = tp1;
 #endif
+#if RTMI_GRID_LDS
+  const GridDesc &G = rtmi_grid_desc;
+#else
   const GridDesc &G = acc_s.grid;
+#endif
   const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
   const float ox = -o.x * ix, oy = -o.y * iy, oz = -o.z * iz;
   // the grid box, clipped to [0, t_max]
@@ -745,6 +764,17 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
       if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[2] += 1;
 #endif
       const uint32_t re = lds_u32(cell + 4u);  // (with the next one: a ds_read2_b32)
+#if RTMI_DEFER_RESOLVE
+      // Deferred root resolution: a lane keeps its first candidate of the
+      // cell and resolves it after the cell's sphere loop (a second candidate
+      // resolves the kept one first).  A wave then runs the resolution once
+      // per cell instead of at every sphere where some lane has a candidate.
+      // The result is the same: resolve_root's acceptance is order-independent
+      // (the closest root, ties to the larger index), and the walk's exit
+      // test comes after the cell's resolutions either way.
+      uint32_t kaddr = 0u;
+      float khb = 0.0f, kdisc = 0.0f;
+#endif
       for (uint32_t r = lds_u32(cell); r < re; r += 4u) {
 #if RTMI_STATS
         gstats[1] += 1;
@@ -754,12 +784,32 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
         float hb, disc;
         sphere_test(lds_sphere(addr), d, K, a, aL, mx, my, mz, hb, disc);
         if (!(disc < 0.0f)) {
+#if RTMI_DEFER_RESOLVE
+          if (kaddr != 0u) {
+#if RTMI_STATS
+            if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
+#endif
+            resolve_root(int32_t((kaddr - base) >> 4), khb, kdisc, inv_a, t_max, best);
+          }
+          kaddr = addr;
+          khb = hb;
+          kdisc = disc;
+#else
 #if RTMI_STATS
           if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
 #endif
           resolve_root(int32_t((addr - base) >> 4), hb, disc, inv_a, t_max, best);
+#endif
         }
       }
+#if RTMI_DEFER_RESOLVE
+      if (kaddr != 0u) {
+#if RTMI_STATS
+        if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
+#endif
+        resolve_root(int32_t((kaddr - base) >> 4), khb, kdisc, inv_a, t_max, best);
+      }
+#endif
       const float texit = __builtin_fminf(tnx, __builtin_fminf(tny, tnz));
       if constexpr (FLAT_Y) {
         // the same step without nested branches: x when its face is nearest

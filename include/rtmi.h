@@ -256,7 +256,13 @@ int rt_render_multi(const rt_scene *scene, const rt_camera *cam, int32_t W, int3
  * sample ranges (each device adds its rows' samples to its own fixed-point
  * accumulator), then rt_multi_accum_resolve gathers the sums (same bits as
  * one rt_render of the covered samples).  rt_multi_context exposes device
- * g's context (tuning, accelerator, counters). */
+ * g's context (tuning, accelerator, counters).
+ * Errors: a call that fails after enqueuing work on some devices waits for
+ * every device's stream before it returns; a failed rt_multi_render_pass (or
+ * rt_multi_accum_reset) leaves the device set without a valid accumulator
+ * (the devices' sums would cover different samples): rt_multi_render_pass and
+ * rt_multi_accum_resolve return RT_EINVAL until the next successful
+ * rt_multi_accum_reset. */
 typedef struct rt_multi rt_multi;
 int rt_multi_create(const rt_scene *scene, int32_t n_gpus, rt_multi **out);
 int rt_multi_destroy(rt_multi *m);

@@ -125,9 +125,6 @@ __device__ unsigned g_trace_n;
 #ifndef RTMI_PERSIST_MIN_BLOCKS
 #define RTMI_PERSIST_MIN_BLOCKS 1
 #endif
-#ifndef RTMI_BLOCK_POOL
-#define RTMI_BLOCK_POOL 0
-#endif
 #ifndef RTMI_PAIR_GROUP
 #define RTMI_PAIR_GROUP 4
 #endif
@@ -357,11 +354,9 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   constexpr int WPB = GridShape<ACC != 0>::waves;
   __shared__ unsigned long long acc[WPB][3][64];
   __shared__ float cam_lds[21];  // the camera (stage_camera)
-  __shared__ int job_next;       // block-shared jobs: the next unclaimed one
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * WPB + wave;
-  if (threadIdx.x == 0) job_next = 0;  // (published by the staging barrier)
   stage_camera(cam_lds, a);
   if constexpr (ACC == 0) __syncthreads();  // (accelerated kernels: stage_* ends with one)
   if constexpr (ACC == 1) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
@@ -382,22 +377,6 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   };
   int tile, s0, ns;
   item_range(item, tile, s0, ns);
-  // Block-shared jobs (RTMI_BLOCK_POOL; block_flush launches, whose block
-  // items are consecutive sample ranges of one tile): the block's waves take
-  // 64-job batches of their items' union from one LDS counter, so no wave runs
-  // out of jobs while its block has some, and the waves ramp down together.
-  // Jobs map to (pixel, sample) as before: the same rays, the same image.
-  const bool shared_jobs = CHUNKED && RTMI_BLOCK_POOL && a.block_flush;
-  if (shared_jobs) {  // the union of the block's items: consecutive sample ranges (the last ones may be empty)
-    const int first = blockIdx.x * WPB, last = min(first + WPB, a.n_items);
-    int t_, n_;
-    item_range(first, t_, s0, ns);
-    for (int it = first + 1; it < last; ++it) {
-      int s_;
-      item_range(it, t_, s_, n_);
-      ns += n_;
-    }
-  }
   if (a.tile_order) tile = a.tile_order[tile];  // expensive tiles first
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
   const int x0 = tx * TW, y0 = ty * TH;
@@ -467,16 +446,9 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   // for the few lanes that regenerate.  Same rays bit for bit.
   V3<float> po, pd;
   Xoro prng;
-  // the next 64 jobs of this wave (wave-private) or of the block (shared)
-  auto claim = [&](int prev) {
-    if (!shared_jobs) return prev + 64;
-    int v = 0;
-    if (lane == 0) v = atomicAdd(&job_next, 64);
-    return __builtin_amdgcn_readfirstlane(v);
-  };
-  int pbase = __builtin_amdgcn_readfirstlane(claim(-64)), ppos = 64;  // wave-uniform: job of slot 0, next unused slot
-  if (pbase < nq) camera_ray(pbase + lane, po, pd, prng);
-  adopt(pbase + lane, po, pd, prng);
+  int pbase = 0, ppos = 64;  // wave-uniform: job of slot 0, next unused slot
+  camera_ray(lane, po, pd, prng);
+  adopt(lane, po, pd, prng);
   auto pull = [](int src4, float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(src4, __float_as_int(v))); };
   auto pull64 = [](int src4, uint64_t v) {
     const uint32_t lo = uint32_t(__builtin_amdgcn_ds_bpermute(src4, int(uint32_t(v))));
@@ -516,7 +488,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
       const int cnt = __popcll(m);
       for (int served = 0; served < cnt;) {
         if (ppos == 64) {
-          pbase = __builtin_amdgcn_readfirstlane(claim(pbase));
+          pbase = __builtin_amdgcn_readfirstlane(pbase + 64);
           ppos = 0;
           if (pbase < nq) camera_ray(pbase + lane, po, pd, prng);
         }
@@ -1008,6 +980,8 @@ struct rt_ctx {
   // only), 1 = probe when no map of this layout exists (default), 2 = probe
   // before every render (no state carried between renders)
   int32_t probe_mode = std::getenv("RTMI_ORDER_PROBE") ? std::atoi(std::getenv("RTMI_ORDER_PROBE")) : 1;
+  // samples per pixel of the probe (RTMI_PROBE_SPP, for A/B; 0 = automatic)
+  int32_t probe_spp = std::getenv("RTMI_PROBE_SPP") ? std::atoi(std::getenv("RTMI_PROBE_SPP")) : 0;
   bool probing = false;
   // automatic item size of the grid kernel: ~want_items items of item_min..125
   // samples (RTMI_WANT_ITEMS / RTMI_ITEM_MIN override, for A/B)
@@ -1754,7 +1728,8 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     if (!ctx->probing && strip && !pass_accum && spp >= 16 &&
         (ctx->probe_mode == 2 || (ctx->probe_mode == 1 && !have_map))) {
       ctx->probing = true;
-      const int rc = render_rows_impl(ctx, cam, W, H, spp >= 256 ? 2 : 1, max_depth, seed, row0, row_step, nrows, strip,
+      const int32_t pspp = ctx->probe_spp > 0 ? std::min(ctx->probe_spp, spp) : (spp >= 256 ? 2 : 1);
+      const int rc = render_rows_impl(ctx, cam, W, H, pspp, max_depth, seed, row0, row_step, nrows, strip,
                                       st, s_base, nullptr);
       ctx->probing = false;
       if (rc) return rc;

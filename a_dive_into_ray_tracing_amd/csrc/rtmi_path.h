@@ -563,6 +563,9 @@ __device__ __forceinline__ float safe_inv(float v) {
 #ifndef RTMI_DEFER_RESOLVE
 #define RTMI_DEFER_RESOLVE 0
 #endif
+#ifndef RTMI_ADDR_TIE
+#define RTMI_ADDR_TIE 0
+#endif
 
 
 #if RTMI_TRACE_PHASES
@@ -758,6 +761,17 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
 #if RTMI_TRACE_PHASES
     tp2 = __builtin_amdgcn_s_memtime();
 #endif
+#if RTMI_ADDR_TIE
+    // The tie rule compares scene indices; in the walk it compares the
+    // spheres' LDS addresses instead (base + 16 x scene index: the same
+    // order), so no index is computed per resolution.  -1: no hit yet.
+    int32_t best_a = best < 0 ? -1 : int32_t(base + 16u * uint32_t(best));
+#define RTMI_WALK_BEST best_a
+#define RTMI_WALK_IDX(addr) int32_t(addr)
+#else
+#define RTMI_WALK_BEST best
+#define RTMI_WALK_IDX(addr) int32_t(((addr) - base) >> 4)
+#endif
     for (;;) {
 #if RTMI_STATS
       gstats[0] += 1;
@@ -789,7 +803,7 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
 #if RTMI_STATS
             if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
 #endif
-            resolve_root(int32_t((kaddr - base) >> 4), khb, kdisc, inv_a, t_max, best);
+            resolve_root(RTMI_WALK_IDX(kaddr), khb, kdisc, inv_a, t_max, RTMI_WALK_BEST);
           }
           kaddr = addr;
           khb = hb;
@@ -798,7 +812,7 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
 #if RTMI_STATS
           if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
 #endif
-          resolve_root(int32_t((addr - base) >> 4), hb, disc, inv_a, t_max, best);
+          resolve_root(RTMI_WALK_IDX(addr), hb, disc, inv_a, t_max, RTMI_WALK_BEST);
 #endif
         }
       }
@@ -807,7 +821,7 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
 #if RTMI_STATS
         if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
 #endif
-        resolve_root(int32_t((kaddr - base) >> 4), khb, kdisc, inv_a, t_max, best);
+        resolve_root(RTMI_WALK_IDX(kaddr), khb, kdisc, inv_a, t_max, RTMI_WALK_BEST);
       }
 #endif
       const float texit = __builtin_fminf(tnx, __builtin_fminf(tny, tnz));
@@ -844,6 +858,11 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
         cell += dcz;
       }
     }
+#if RTMI_ADDR_TIE
+    best = best_a < 0 ? -1 : int32_t((uint32_t(best_a) - base) >> 4);
+#endif
+#undef RTMI_WALK_BEST
+#undef RTMI_WALK_IDX
   }
 #if RTMI_TRACE_PHASES
   {

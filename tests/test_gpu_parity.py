@@ -573,6 +573,30 @@ def test_cost_ordered_dispatch_same_image(kernel, accel, final_world, final_rend
     assert np.array_equal(ordered, want)
 
 
+@pytest.mark.parametrize("probe_spp", ["1", "2", "5"])
+def test_probe_samples_do_not_change_the_image(probe_spp, final_world, monkeypatch):
+    """The cost probe of a one-shot render (RTMI_PROBE_SPP samples per pixel
+    into the output, counting world.hit per tile) only orders the tiles: the
+    image and the world.hit count of the render equal the unordered render's
+    and the oracle's, whatever the probe's sample count."""
+    W, H, S = 64, 40, 20
+    cam = rt.final_camera(W / H)
+    monkeypatch.setenv("RTMI_PROBE_SPP", probe_spp)
+    r = rt.Renderer(final_world, 0)
+    try:
+        r.set_accel("grid")
+        r.set_ordering("none")
+        plain = r.render(cam, W, H, S, 50, SEED)
+        plain_segs = r.last_segments()
+        r.set_ordering("cost")  # no map of this layout: probe first
+        got = r.render(cam, W, H, S, 50, SEED)
+        segs = r.last_segments()
+    finally:
+        r.close()
+    assert np.array_equal(got, plain) and segs == plain_segs
+    assert np.array_equal(got, O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED))
+
+
 @pytest.mark.parametrize("accel", ["none", "bvh", "grid"])
 @pytest.mark.parametrize("W,H,S", [(40, 24, 37), (29, 19, 37), (29, 19, 5)])
 def test_block_flush_same_image(accel, W, H, S, final_world, monkeypatch):

@@ -517,19 +517,13 @@ __host__ __device__ constexpr size_t grid_lds_bytes(int32_t nsph, int32_t ncells
   return size_t(nsph) * 16 + (size_t(ncells) + 1) * 4 + size_t(nrefs) * 4;
 }
 
-#ifndef RTMI_GRID_LDS
-#define RTMI_GRID_LDS 0
-#endif
-#if RTMI_GRID_LDS
 // The grid descriptor in LDS (staged with the grid): the walk setup reads its
-// fields there instead of holding them in scalar registers, which overflow the
-// kernel's SGPR budget into VGPR lanes read back with v_readlane.
+// fields there instead of holding them in scalar registers, which overflowed
+// the kernel's SGPR budget into VGPR lanes read back with v_readlane (15 per
+// loop pass, 3 now; config 2 -0.6 to -0.8%, profiles/r04/ab_variants*.txt).
 __shared__ GridDesc rtmi_grid_desc;
-#endif
 __device__ __forceinline__ void stage_grid(const Accel &g) {
-#if RTMI_GRID_LDS
   if (threadIdx.x == 0) rtmi_grid_desc = g.grid;
-#endif
   for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) rtmi_bvh_lds[i] = g.sph[i];
   uint32_t *c = reinterpret_cast<uint32_t *>(rtmi_bvh_lds + g.nsph);
   uint32_t *r = c + g.grid.ncells + 1;
@@ -559,12 +553,6 @@ __device__ __forceinline__ float safe_inv(float v) {
 
 #ifndef RTMI_TRACE_PHASES
 #define RTMI_TRACE_PHASES 0
-#endif
-#ifndef RTMI_DEFER_RESOLVE
-#define RTMI_DEFER_RESOLVE 0
-#endif
-#ifndef RTMI_ADDR_TIE
-#define RTMI_ADDR_TIE 0
 #endif
 
 
@@ -703,11 +691,7 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
   pc.c[0] += tp1 - tp0;
   unsigned long long tp2 = tp1;
 #endif
-#if RTMI_GRID_LDS
-  const GridDesc &G = rtmi_grid_desc;
-#else
-  const GridDesc &G = acc_s.grid;
-#endif
+  const GridDesc &G = rtmi_grid_desc;  // (stage_grid)
   const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
   const float ox = -o.x * ix, oy = -o.y * iy, oz = -o.z * iz;
   // the grid box, clipped to [0, t_max]
@@ -761,34 +745,27 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
 #if RTMI_TRACE_PHASES
     tp2 = __builtin_amdgcn_s_memtime();
 #endif
-#if RTMI_ADDR_TIE
     // The tie rule compares scene indices; in the walk it compares the
     // spheres' LDS addresses instead (base + 16 x scene index: the same
     // order), so no index is computed per resolution.  -1: no hit yet.
     int32_t best_a = best < 0 ? -1 : int32_t(base + 16u * uint32_t(best));
-#define RTMI_WALK_BEST best_a
-#define RTMI_WALK_IDX(addr) int32_t(addr)
-#else
-#define RTMI_WALK_BEST best
-#define RTMI_WALK_IDX(addr) int32_t(((addr) - base) >> 4)
-#endif
     for (;;) {
 #if RTMI_STATS
       gstats[0] += 1;
       if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[2] += 1;
 #endif
       const uint32_t re = lds_u32(cell + 4u);  // (with the next one: a ds_read2_b32)
-#if RTMI_DEFER_RESOLVE
       // Deferred root resolution: a lane keeps its first candidate of the
       // cell and resolves it after the cell's sphere loop (a second candidate
-      // resolves the kept one first).  A wave then runs the resolution once
-      // per cell instead of at every sphere where some lane has a candidate.
+      // resolves the kept one first).  A wave then runs the resolution about
+      // once per cell instead of at every sphere where some lane has a
+      // candidate (tools/grid_sim.c: 3.4 instead of 4.8 per wave-segment).
       // The result is the same: resolve_root's acceptance is order-independent
       // (the closest root, ties to the larger index), and the walk's exit
-      // test comes after the cell's resolutions either way.
+      // test comes after the cell's resolutions either way.  (0: none; every
+      // sphere address is above the kernel's static LDS.)
       uint32_t kaddr = 0u;
       float khb = 0.0f, kdisc = 0.0f;
-#endif
       for (uint32_t r = lds_u32(cell); r < re; r += 4u) {
 #if RTMI_STATS
         gstats[1] += 1;
@@ -798,32 +775,23 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
         float hb, disc;
         sphere_test(lds_sphere(addr), d, K, a, aL, mx, my, mz, hb, disc);
         if (!(disc < 0.0f)) {
-#if RTMI_DEFER_RESOLVE
           if (kaddr != 0u) {
 #if RTMI_STATS
             if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
 #endif
-            resolve_root(RTMI_WALK_IDX(kaddr), khb, kdisc, inv_a, t_max, RTMI_WALK_BEST);
+            resolve_root(int32_t(kaddr), khb, kdisc, inv_a, t_max, best_a);
           }
           kaddr = addr;
           khb = hb;
           kdisc = disc;
-#else
-#if RTMI_STATS
-          if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
-#endif
-          resolve_root(RTMI_WALK_IDX(addr), hb, disc, inv_a, t_max, RTMI_WALK_BEST);
-#endif
         }
       }
-#if RTMI_DEFER_RESOLVE
       if (kaddr != 0u) {
 #if RTMI_STATS
         if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
 #endif
-        resolve_root(RTMI_WALK_IDX(kaddr), khb, kdisc, inv_a, t_max, RTMI_WALK_BEST);
+        resolve_root(int32_t(kaddr), khb, kdisc, inv_a, t_max, best_a);
       }
-#endif
       const float texit = __builtin_fminf(tnx, __builtin_fminf(tny, tnz));
       if constexpr (FLAT_Y) {
         // the same step without nested branches: x when its face is nearest
@@ -858,11 +826,7 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
         cell += dcz;
       }
     }
-#if RTMI_ADDR_TIE
     best = best_a < 0 ? -1 : int32_t((uint32_t(best_a) - base) >> 4);
-#endif
-#undef RTMI_WALK_BEST
-#undef RTMI_WALK_IDX
   }
 #if RTMI_TRACE_PHASES
   {

@@ -1,5 +1,6 @@
 """Summarise rocprofv3 PMC csvs of the render kernels: per-dispatch means,
-grouped by kernel (render and finalize kernels).  usage: pmc_summary.py DIR"""
+grouped by kernel (render and finalize kernels); "renders" leaves out dispatches
+below a quarter of the largest (the cost probe).  usage: pmc_summary.py DIR"""
 import collections
 import csv
 import glob
@@ -21,4 +22,7 @@ for k in sorted(vals):
     print(k)
     for c in sorted(vals[k]):
         v = vals[k][c]
-        print(f"  {c:32s} mean {sum(v)/len(v):.4g}  (n={len(v)})")
+        # the renders proper: a one-shot render's cost probe (a few spp, the
+        # same kernel) is a dispatch far smaller than the rest
+        big = [x for x in v if x >= 0.25 * max(v)] if max(v) > 0 else v
+        print(f"  {c:32s} mean {sum(v)/len(v):.4g}  (n={len(v)})  renders {sum(big)/len(big):.4g}  (n={len(big)})")

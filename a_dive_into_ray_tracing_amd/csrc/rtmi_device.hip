@@ -125,6 +125,12 @@ __device__ unsigned g_trace_n;
 #ifndef RTMI_PERSIST_MIN_BLOCKS
 #define RTMI_PERSIST_MIN_BLOCKS 1
 #endif
+#ifndef RTMI_RAMP_PRIO
+#define RTMI_RAMP_PRIO 0
+#endif
+#ifndef RTMI_BASE_PRIO
+#define RTMI_BASE_PRIO 0
+#endif
 #ifndef RTMI_PAIR_GROUP
 #define RTMI_PAIR_GROUP 4
 #endif
@@ -446,6 +452,9 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   // for the few lanes that regenerate.  Same rays bit for bit.
   V3<float> po, pd;
   Xoro prng;
+#if RTMI_BASE_PRIO
+  __builtin_amdgcn_s_setprio(RTMI_BASE_PRIO);
+#endif
   int pbase = 0, ppos = 64;  // wave-uniform: job of slot 0, next unused slot
   camera_ray(lane, po, pd, prng);
   adopt(lane, po, pd, prng);
@@ -491,6 +500,9 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
           pbase = __builtin_amdgcn_readfirstlane(pbase + 64);
           ppos = 0;
           if (pbase < nq) camera_ray(pbase + lane, po, pd, prng);
+#if RTMI_RAMP_PRIO != RTMI_BASE_PRIO
+          else __builtin_amdgcn_s_setprio(RTMI_RAMP_PRIO);  // the item's jobs are all taken: ramp-down
+#endif
         }
         const int take = min(cnt - served, 64 - ppos);
         const int r = rank - served;

@@ -125,9 +125,6 @@ __device__ unsigned g_trace_n;
 #ifndef RTMI_PERSIST_MIN_BLOCKS
 #define RTMI_PERSIST_MIN_BLOCKS 1
 #endif
-#ifndef RTMI_BLOCK_POOL
-#define RTMI_BLOCK_POOL 0
-#endif
 #ifndef RTMI_SYNC_PROBE
 #define RTMI_SYNC_PROBE 0
 #endif
@@ -360,10 +357,6 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   constexpr int WPB = GridShape<ACC != 0>::waves;
   __shared__ unsigned long long acc[WPB][3][64];
   __shared__ float cam_lds[21];  // the camera (stage_camera)
-#if RTMI_BLOCK_POOL
-  __shared__ int job_next;  // block-shared jobs: the next unclaimed one
-  if (threadIdx.x == 0) job_next = 0;  // (published by the staging barrier)
-#endif
 #if RTMI_SYNC_PROBE
   __shared__ int blk_any[2];
   if (threadIdx.x < 2) blk_any[threadIdx.x] = 0;  // (published by the staging barrier)
@@ -397,24 +390,6 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   int tile, s0, ns;
   item_range(has_item ? item : 0, tile, s0, ns);
   if (!has_item) ns = 0;
-#if RTMI_BLOCK_POOL
-  // Block-shared jobs (analysis variant; block_flush launches, whose block
-  // items are consecutive sample ranges of one tile): the block's waves take
-  // 64-job batches of their items' union from one LDS counter, each claim
-  // issued one batch ahead so its latency is hidden, and the waves end
-  // together.  Same (pixel, sample) jobs, same image.
-  const bool shared_jobs = CHUNKED && a.block_flush;
-  if (shared_jobs) {
-    const int first = blockIdx.x * WPB, last = min(first + WPB, a.n_items);
-    int t_, n_;
-    item_range(first, t_, s0, ns);
-    for (int it = first + 1; it < last; ++it) {
-      int s_;
-      item_range(it, t_, s_, n_);
-      ns += n_;
-    }
-  }
-#endif
   if (a.tile_order) tile = a.tile_order[tile];  // expensive tiles first
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
   const int x0 = tx * TW, y0 = ty * TH;
@@ -484,18 +459,9 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   // for the few lanes that regenerate.  Same rays bit for bit.
   V3<float> po, pd;
   Xoro prng;
-#if RTMI_BLOCK_POOL
-  int pnext = 0;  // lane 0: the batch claimed for the next refill
-  if (shared_jobs && lane == 0) pnext = atomicAdd(&job_next, 64);
-  int pbase = shared_jobs ? __builtin_amdgcn_readfirstlane(pnext) : 0, ppos = 64;
-  if (shared_jobs && lane == 0) pnext = atomicAdd(&job_next, 64);
-  if (pbase < nq) camera_ray(pbase + lane, po, pd, prng);
-  adopt(pbase + lane, po, pd, prng);
-#else
   int pbase = 0, ppos = 64;  // wave-uniform: job of slot 0, next unused slot
   camera_ray(lane, po, pd, prng);
   adopt(lane, po, pd, prng);
-#endif
   auto pull = [](int src4, float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(src4, __float_as_int(v))); };
   auto pull64 = [](int src4, uint64_t v) {
     const uint32_t lo = uint32_t(__builtin_amdgcn_ds_bpermute(src4, int(uint32_t(v))));
@@ -552,16 +518,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
       const int cnt = __popcll(m);
       for (int served = 0; served < cnt;) {
         if (ppos == 64) {
-#if RTMI_BLOCK_POOL
-          if (shared_jobs) {
-            pbase = __builtin_amdgcn_readfirstlane(pnext);
-            if (lane == 0) pnext = atomicAdd(&job_next, 64);
-          } else {
-            pbase = __builtin_amdgcn_readfirstlane(pbase + 64);
-          }
-#else
           pbase = __builtin_amdgcn_readfirstlane(pbase + 64);
-#endif
           ppos = 0;
           if (pbase < nq) camera_ray(pbase + lane, po, pd, prng);
         }

@@ -21,16 +21,19 @@ def strip_rows(H, rank, world):
     return rank, world, (H + world - 1) // world
 
 
-def gather_strips(strip, rank, world, dst=0):
+def gather_strips(strip, rank, world, dst=0, async_op=False):
     """Gather every rank's strip tensor to `dst` (one collective).  Returns the
-    list of strips on dst, None elsewhere."""
+    list of strips on dst, None elsewhere; with async_op, (that list, the
+    collective's Work): the strips are valid, and `strip` may be overwritten,
+    only after Work.wait() (for RCCL that makes the caller's current stream
+    wait for the collective, without blocking the host)."""
     import torch.distributed as dist
 
     if world == 1:
-        return [strip]
+        return ([strip], None) if async_op else [strip]
     bufs = [strip.new_empty(strip.shape) for _ in range(world)] if rank == dst else None
-    dist.gather(strip, gather_list=bufs, dst=dst)
-    return bufs
+    work = dist.gather(strip, gather_list=bufs, dst=dst, async_op=async_op)
+    return (bufs, work) if async_op else bufs
 
 
 def unpermute(strips, H):

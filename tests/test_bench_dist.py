@@ -39,6 +39,7 @@ def test_bench_n_ranks_line_schema(n, tmp_path):
     # (800 rows are ragged over 3 ranks: padded strips count nothing)
     assert sum(di["segments_per_rank"]) == 1200 * 800 * 500
     assert di["kernel_imbalance"] >= 1.0
+    assert "overlap" in di["gather_note"]  # timed steps: gather k overlaps render k+1 (two buffers)
     gc = d["gather_check"]
     assert gc["rows"] == 800 and gc["bit_exact_vs_1gpu_frame"] is True and gc["max_abs_diff"] == 0.0
     assert "cpu_baseline" not in d  # rank 0 at N = 1 only

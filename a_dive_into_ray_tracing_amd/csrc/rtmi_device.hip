@@ -125,6 +125,9 @@ __device__ unsigned g_trace_n;
 #ifndef RTMI_PERSIST_MIN_BLOCKS
 #define RTMI_PERSIST_MIN_BLOCKS 1
 #endif
+#ifndef RTMI_BLOCK_COUNTS
+#define RTMI_BLOCK_COUNTS 1
+#endif
 #ifndef RTMI_SYNC_PROBE
 #define RTMI_SYNC_PROBE 0
 #endif
@@ -357,6 +360,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   constexpr int WPB = GridShape<ACC != 0>::waves;
   __shared__ unsigned long long acc[WPB][3][64];
   __shared__ float cam_lds[21];  // the camera (stage_camera)
+  __shared__ unsigned blk_seg[WPB];  // the waves' world.hit counts (block_flush)
 #if RTMI_SYNC_PROBE
   __shared__ int blk_any[2];
   if (threadIdx.x < 2) blk_any[threadIdx.x] = 0;  // (published by the staging barrier)
@@ -543,9 +547,17 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
 #endif
   }
 
+  // world.hit count and tile cost: per wave, or (block_flush: the block's
+  // waves share the tile) summed in LDS and added once per block at the
+  // flush — 30 000 instead of 120 000 single-lane global atomics at config 2
+  const bool block_counts = CHUNKED && RTMI_BLOCK_COUNTS && a.block_flush;
   if (lane == 0) {
-    atomicAdd(segments, (unsigned long long)nseg);
-    if (a.tile_cost) atomicAdd(&a.tile_cost[tile], nseg);
+    if (block_counts) {
+      blk_seg[wave] = nseg;
+    } else {
+      atomicAdd(segments, (unsigned long long)nseg);
+      if (a.tile_cost) atomicAdd(&a.tile_cost[tile], nseg);
+    }
   }
   flush_counters(cnt, lane, segments);
 #if RTMI_TRACE_PHASES
@@ -565,6 +577,13 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   if constexpr (CHUNKED) {
     if (a.block_flush) {  // block-uniform; no wave of this block returned early
       __syncthreads();
+      if (block_counts && threadIdx.x == 0) {
+        unsigned bseg = 0;
+#pragma unroll
+        for (int w = 0; w < WPB; ++w) bseg += blk_seg[w];
+        atomicAdd(segments, (unsigned long long)bseg);
+        if (a.tile_cost) atomicAdd(&a.tile_cost[tile], bseg);
+      }
       if (wave == 0 && fl < nv) {
         const int ly = fl / vw, lx = fl - ly * vw;
         const size_t o3 = (size_t(y0 + ly) * size_t(a.W) + size_t(x0 + lx)) * 3;

@@ -554,9 +554,6 @@ __device__ __forceinline__ float safe_inv(float v) {
 #ifndef RTMI_TRACE_PHASES
 #define RTMI_TRACE_PHASES 0
 #endif
-#ifndef RTMI_BIG_DEFER
-#define RTMI_BIG_DEFER 0
-#endif
 
 
 #if RTMI_TRACE_PHASES
@@ -645,34 +642,10 @@ __device__ __forceinline__ void hit_big(const Accel &acc_s, V3<float> d, float K
 #if RTMI_STATS
       if (__lane_id() == __builtin_ctzll(__ballot(1))) stats[4] += 1;
 #endif
-#if RTMI_BIG_DEFER
-      // deferred, as the grid walk's cells: a lane keeps its first candidate
-      // and resolves it when a second one comes (slot 0 — the final scene's
-      // ground, a candidate for nearly every ray — last), then at the end
-      // (the kept slot's hb and disc are selected from the group's results,
-      // still live, rather than copied: no extra registers)
-      int32_t kb = -1;  // kept slot within the group, 0..3
-      auto sel = [&](int32_t b, f2v v0, f2v v1) { return b == 0 ? v0.x : (b == 1 ? v0.y : (b == 2 ? v1.x : v1.y)); };
-      auto flush = [&]() {
-        if (kb >= 0) resolve_root(big_index(acc_s, 2 * q + kb), sel(kb, hb0, hb1), sel(kb, d0, d1), inv_a, t_max, best);
-      };
-      auto keep = [&](int32_t b) {
-        if (m & (1u << b)) {
-          flush();
-          kb = b;
-        }
-      };
-      keep(1);
-      keep(2);
-      keep(3);
-      keep(0);
-      flush();
-#else
       if (m & 1u) resolve_root(big_index(acc_s, 2 * q), hb0.x, d0.x, inv_a, t_max, best);
       if (m & 2u) resolve_root(big_index(acc_s, 2 * q + 1), hb0.y, d0.y, inv_a, t_max, best);
       if (m & 4u) resolve_root(big_index(acc_s, 2 * q + 2), hb1.x, d1.x, inv_a, t_max, best);
       if (m & 8u) resolve_root(big_index(acc_s, 2 * q + 3), hb1.y, d1.y, inv_a, t_max, best);
-#endif
     }
   }
 }

@@ -125,9 +125,6 @@ __device__ unsigned g_trace_n;
 #ifndef RTMI_PERSIST_MIN_BLOCKS
 #define RTMI_PERSIST_MIN_BLOCKS 1
 #endif
-#ifndef RTMI_BLOCK_COUNTS
-#define RTMI_BLOCK_COUNTS 1
-#endif
 #ifndef RTMI_SYNC_PROBE
 #define RTMI_SYNC_PROBE 0
 #endif
@@ -550,7 +547,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   // world.hit count and tile cost: per wave, or (block_flush: the block's
   // waves share the tile) summed in LDS and added once per block at the
   // flush — 30 000 instead of 120 000 single-lane global atomics at config 2
-  const bool block_counts = CHUNKED && RTMI_BLOCK_COUNTS && a.block_flush;
+  const bool block_counts = CHUNKED && a.block_flush;
   if (lane == 0) {
     if (block_counts) {
       blk_seg[wave] = nseg;

@@ -69,6 +69,9 @@ struct RenderArgs {
   // tile's float sums straight to the output strip — no accumulator memset,
   // global atomics or finalize pass (config 2: 500 spp = 4 items of 125)
   int32_t block_owns_tile;
+  // the fixed-point accumulators' byte offset in the dynamic LDS (past the
+  // acceleration structure; launch_tw)
+  int32_t acc_off;
   // progressive passes: this launch renders samples s_base + [0, spp)
   int32_t s_base;
   uint64_t out_elems;  // elements of accum / out (RTMI_CHECK builds verify every write)
@@ -276,6 +279,7 @@ __device__ __forceinline__ bool path_segment(const SceneView<float> &sc, const S
   const unsigned long long cyc0 = __builtin_amdgcn_s_memtime();
 #endif
   int k;
+  uint32_t key = 0u;  // the grid's hit slot (hit_world_grid)
   if constexpr (ACC == 1) {
     k = hit_world_bvh<kBigGroup>(a.acc, o, d, t
 #if RTMI_STATS
@@ -283,7 +287,7 @@ __device__ __forceinline__ bool path_segment(const SceneView<float> &sc, const S
 #endif
     );
   } else if constexpr (ACC >= 2) {
-    k = hit_world_grid<kBigGroup, ACC == 3>(a.acc, o, d, t
+    k = hit_world_grid<kBigGroup, ACC == 3>(a.acc, o, d, t, key
 #if RTMI_STATS
                                    , cnt.bvh_stats
 #endif
@@ -310,11 +314,11 @@ __device__ __forceinline__ bool path_segment(const SceneView<float> &sc, const S
   // the hit sphere's three records in one memory round trip (a miss reads
   // sphere 0's, unused)
   const int kk = miss ? 0 : k;
-  // the grid kernels hold every sphere's {c, S} in LDS at its scene index
-  // (stage_grid): the hit record's geometry from there, one global gather
-  // fewer (19.82 -> 19.73 ms, profiles/r03/ab_geom_lds.txt)
+  // the grid kernels hold the hit sphere's {c, S} in LDS at the hit's record
+  // slot (stage_grid): the hit record's geometry from there, one global
+  // gather fewer (19.82 -> 19.73 ms, profiles/r03/ab_geom_lds.txt)
   const float4 sh1k = sc.sh1[kk], sh0k = sc.sh0[kk];
-  const float4 geomk = ACC >= 2 ? lds_sphere(lds_address(rtmi_bvh_lds) + 16u * uint32_t(kk)) : sc.geom[kk];
+  const float4 geomk = ACC >= 2 ? lds_sphere(key) : sc.geom[kk];
   const int kind = miss ? -1 : int(sh1k.x);
   float inv_len = 0.0f;
   if (kind != RT_MAT_LAMBERTIAN) inv_len = drcp(dsqrt(dot<true>(d, d)));
@@ -355,7 +359,6 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
     float *__restrict__ out, unsigned long long *__restrict__ segments) {
   constexpr int TH = 64 / TW;
   constexpr int WPB = GridShape<ACC != 0>::waves;
-  __shared__ unsigned long long acc[WPB][3][64];
   __shared__ float cam_lds[21];  // the camera (stage_camera)
   __shared__ unsigned blk_seg[WPB];  // the waves' world.hit counts (block_flush)
 #if RTMI_SYNC_PROBE
@@ -365,6 +368,17 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * WPB + wave;
+  // The per-pixel int64 fixed-point sums, in the dynamic LDS past the
+  // acceleration structure: one set per wave, or (block_flush: the block's
+  // waves share one tile) one set the four waves add into together — integer
+  // sums, so the same bits in any order, and 4.5 KB less LDS per block, which
+  // keeps 8 blocks per CU with the grid's record slots (grid_lds_bytes).
+  // Zeroed before the staging barrier, which publishes it.
+  const bool acc_shared = CHUNKED && a.block_flush;
+  unsigned long long *const acc_lds =
+      reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(rtmi_bvh_lds) + a.acc_off);
+  for (int i = threadIdx.x; i < (acc_shared ? 3 * 64 : WPB * 3 * 64); i += 64 * WPB) acc_lds[i] = 0;
+  unsigned long long *const acc = acc_lds + (acc_shared ? 0 : wave * 3 * 64);  // [3][64]
   stage_camera(cam_lds, a);
   if constexpr (ACC == 0) __syncthreads();  // (accelerated kernels: stage_* ends with one)
   if constexpr (ACC == 1) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
@@ -398,9 +412,6 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   const int nv = vw * vh;  // valid pixels of this tile
   const int nq = nv * ns;  // jobs: (pixel, sample) pairs of this item
 
-  acc[wave][0][lane] = 0;
-  acc[wave][1][lane] = 0;
-  acc[wave][2][lane] = 0;
   unsigned nseg = 0;  // world.hit calls of this wave (wave-uniform; algorithmic-work accounting)
   RTMI_TRACE_BEGIN
   SegCounters cnt{};
@@ -508,9 +519,9 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
     if (m) {
       if (done) {
         const int px = pxd >> 24;
-        atomicAdd(&acc[wave][0][px], (unsigned long long)to_fixed(col.x));
-        atomicAdd(&acc[wave][1][px], (unsigned long long)to_fixed(col.y));
-        atomicAdd(&acc[wave][2][px], (unsigned long long)to_fixed(col.z));
+        atomicAdd(&acc[px], (unsigned long long)to_fixed(col.x));
+        atomicAdd(&acc[64 + px], (unsigned long long)to_fixed(col.y));
+        atomicAdd(&acc[128 + px], (unsigned long long)to_fixed(col.z));
       }
       const int rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
       // ranks [0, cnt) take slots ppos, ppos + 1, ...: at most two rounds,
@@ -585,9 +596,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
         const int ly = fl / vw, lx = fl - ly * vw;
         const size_t o3 = (size_t(y0 + ly) * size_t(a.W) + size_t(x0 + lx)) * 3;
         for (int c = 0; c < 3; ++c) {
-          unsigned long long v = 0;
-#pragma unroll
-          for (int w = 0; w < WPB; ++w) v += acc[w][c][fl];
+          const unsigned long long v = acc[64 * c + fl];  // (acc_shared: the block's sums)
           if (a.block_owns_tile) out[o3 + c] = from_fixed((long long)v);
           else atomicAdd(&accum[o3 + c], v);
         }
@@ -605,7 +614,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
     } else
 #endif
     for (int c = 0; c < 3; ++c) {
-      const unsigned long long v = acc[wave][c][fl];
+      const unsigned long long v = acc[64 * c + fl];
       if constexpr (CHUNKED) atomicAdd(&accum[o3 + c], v);
       else out[o3 + c] = from_fixed((long long)v);
     }
@@ -859,17 +868,18 @@ __global__ __launch_bounds__(256) void debug_hit_kernel(const SpherePair *__rest
   const V3<float> o = mk(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
   const V3<float> d = mk(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
   float t0, t1;
+  uint32_t key;
 #if RTMI_STATS
   unsigned st[4] = {0, 0, 0, 0}, bst[5] = {0, 0, 0, 0, 0};
   out_idx[2 * i] = hit_world_packed<kPairGroup>(pairs, npairs, o, d, t0, st);
-  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1, bst) : hit_world_grid<kBigGroup, ACC == 3>(acc, o, d, t1, bst);
+  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1, bst) : hit_world_grid<kBigGroup, ACC == 3>(acc, o, d, t1, key, bst);
 #else
   out_idx[2 * i] = hit_world_packed<kPairGroup>(pairs, npairs, o, d, t0);
 #if RTMI_TRACE_PHASES
   PhaseClock pc{{0, 0, 0}};
-  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup, ACC == 3>(acc, o, d, t1, pc);
+  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup, ACC == 3>(acc, o, d, t1, key, pc);
 #else
-  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup, ACC == 3>(acc, o, d, t1);
+  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup, ACC == 3>(acc, o, d, t1, key);
 #endif
 #endif
   out_t[2 * i] = t0;
@@ -1263,7 +1273,8 @@ struct GridBuild {
   std::vector<uint32_t> cells;  // ncells + 1: each cell's first reference
   std::vector<uint32_t> refs;   // 16 x scene index
 };
-bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, int32_t n, GridBuild &out) {
+bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, int32_t n, int32_t nbig_slots,
+                GridBuild &out) {
   if (n > 65535) return false;  // references are 16-bit scene indices
   const char *env = std::getenv("RTMI_GRID_CELLS");
   // 0.3 cells per sphere: config 2 33.3 ms (0.2: 33.3, 0.5: 33.6, 1: 34.5,
@@ -1325,7 +1336,9 @@ bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, int32_t 
   }
   out.cells[size_t(total)] = uint32_t(out.refs.size());
   out.desc.nrefs = int32_t(out.refs.size());
-  return grid_lds_bytes(int32_t(out.sph.size()), out.desc.ncells, out.desc.nrefs) <= kBvhLdsMax;
+  out.desc.cells_off = 16u * uint32_t(nbig_slots + out.desc.nrefs);  // grid_lds_bytes' layout
+  out.desc.idx_off = out.desc.cells_off + 4u * uint32_t(out.desc.ncells + 1);
+  return grid_lds_bytes(nbig_slots, out.desc.ncells, out.desc.nrefs) <= kBvhLdsMax;
 }
 }  // namespace
 
@@ -1466,7 +1479,7 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
     // uniform grid over the same small spheres
     ctx->grid_ok = false;
     GridBuild gb;
-    if (!small.empty() && build_grid(b, small, n, gb)) {
+    if (!small.empty() && build_grid(b, small, n, nb_pad, gb)) {
       if ((rc = dev_alloc(&ctx->grid_sph, gb.sph.size())) || (rc = dev_alloc(&ctx->grid_cells, gb.cells.size())) ||
           (rc = dev_alloc(&ctx->grid_refs, std::max<size_t>(gb.refs.size(), 1))))
         return rc;
@@ -1490,7 +1503,7 @@ RTMI_EXPORT int rt_ctx_grid_info(rt_ctx *ctx, int32_t *dims3, int32_t *n_refs, i
   if (!ctx->grid_ok) return set_error(RT_EUNSUPPORTED, "no grid for this scene");
   if (dims3) for (int a = 0; a < 3; ++a) dims3[a] = ctx->grid.n[a];
   if (n_refs) *n_refs = ctx->grid.nrefs;
-  if (lds_bytes) *lds_bytes = int32_t(grid_lds_bytes(ctx->ngrid_sph, ctx->grid.ncells, ctx->grid.nrefs));
+  if (lds_bytes) *lds_bytes = int32_t(grid_lds_bytes(2 * ctx->nbig_pairs, ctx->grid.ncells, ctx->grid.nrefs));
   return RT_OK;
 }
 
@@ -1537,7 +1550,7 @@ namespace {
 
 size_t accel_lds_bytes(const Accel &acc, int kind) {
   if (kind == 1) return bvh_lds_bytes(acc.nnodes, acc.nsph);
-  if (kind >= 2) return grid_lds_bytes(acc.nsph, acc.grid.ncells, acc.grid.nrefs);
+  if (kind >= 2) return grid_lds_bytes(2 * acc.nbig_pairs, acc.grid.ncells, acc.grid.nrefs);
   return 0;
 }
 
@@ -1573,13 +1586,17 @@ void launch_persistent(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ct
 template <int TW, int ACC>
 void launch_tw(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a,
                unsigned long long *accum, float *out) {
-  const size_t lds = accel_lds_bytes(a.acc, ACC);
+  // dynamic LDS: the structure, then the accumulators (render_kernel: one
+  // set per block with block_flush, else one per wave)
+  RenderArgs b = a;
+  b.acc_off = int32_t((accel_lds_bytes(a.acc, ACC) + 15) / 16 * 16);
+  const size_t lds = size_t(b.acc_off) + size_t(chunked && a.block_flush ? 1 : GridShape<ACC != 0>::waves) * 3 * 64 * 8;
   if (chunked)
     hipLaunchKernelGGL((render_kernel<TW, true, ACC>), grid, dim3(64 * GridShape<ACC != 0>::waves), lds, st, ctx->geom,
-                       ctx->sh0, ctx->sh1, ctx->pairs, a, accum, out, ctx->segments);
+                       ctx->sh0, ctx->sh1, ctx->pairs, b, accum, out, ctx->segments);
   else
     hipLaunchKernelGGL((render_kernel<TW, false, ACC>), grid, dim3(64 * GridShape<ACC != 0>::waves), lds, st, ctx->geom,
-                       ctx->sh0, ctx->sh1, ctx->pairs, a, accum, out, ctx->segments);
+                       ctx->sh0, ctx->sh1, ctx->pairs, b, accum, out, ctx->segments);
 }
 
 template <int TW>

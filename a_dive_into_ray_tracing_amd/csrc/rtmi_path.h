@@ -441,18 +441,16 @@ static_assert(kLeafMax >= 1 && kLeafMax <= 15, "leaf size");
 // Uniform grid over the small spheres (RT_ACCEL_GRID): cells
 // of size h over the box g0 + [0, n*h) of the spheres' margin-grown boxes.
 // Cell c lists refs[cells[c] .. cells[c+1]): every sphere whose grown box
-// overlaps it, as the byte offset (16 x scene index) of its record in the
-// grid's LDS sphere array, which holds every sphere of the scene at its scene
-// index (the big spheres' slots unused): a tie compares scene indices
-// directly.  In LDS (stage_grid) both arrays hold absolute LDS addresses, so
-// the walk does no address arithmetic: one ds_read2_b32 gives a cell's
-// reference range, one ds_read_b32 a reference, one ds_read_b128 the sphere.
+// overlaps it, as 16 x its scene index.  In LDS (stage_grid) each reference
+// becomes a copy of its sphere's record, so the walk reads a sphere with one
+// ds_read_b128 at the reference itself (grid_lds_bytes).
 struct GridDesc {
   float g0[3], h[3], inv_h[3], g1[3];  // origin, cell size, 1/h, far corner
   int32_t n[3];
   int32_t ncells, nrefs;
   const uint32_t *cells;  // ncells + 1 first-reference indices
   const uint32_t *refs;
+  uint32_t cells_off, idx_off;  // in LDS: the cell starts and the slot indices, bytes past the slots
 };
 
 struct Accel {
@@ -511,10 +509,16 @@ __device__ __forceinline__ float4 lds_sphere(uint32_t addr) {
 #endif
 }
 
-// Grid LDS layout: nsph sphere float4s (scene order), ncells + 1 uint32 cell
-// starts, nrefs uint32 references — all addresses absolute LDS addresses.
-__host__ __device__ constexpr size_t grid_lds_bytes(int32_t nsph, int32_t ncells, int32_t nrefs) {
-  return size_t(nsph) * 16 + (size_t(ncells) + 1) * 4 + size_t(nrefs) * 4;
+// Grid LDS layout ("record slots"): one 16-byte sphere record {c, S} per slot
+// — first the big spheres' slots (2 x nbig_pairs, dummies included), then
+// every cell's references in cell order, each a copy of the record of the
+// sphere it lists — then ncells + 1 uint32 cell starts (the LDS addresses of
+// their first slots), then one uint16 scene index per slot.  The walk reads a
+// sphere with one ds_read_b128 at the slot (no reference indirection), and
+// names a hit by its slot's LDS address (a "key"); the scene index is read
+// from the index table only for an exact tie and once at the walk's end.
+__host__ __device__ constexpr size_t grid_lds_bytes(int32_t nbig_slots, int32_t ncells, int32_t nrefs) {
+  return size_t(nbig_slots + nrefs) * 16 + (size_t(ncells) + 1) * 4 + (size_t(nbig_slots + nrefs) * 2 + 3) / 4 * 4;
 }
 
 // The grid descriptor in LDS (staged with the grid): the walk setup reads its
@@ -523,19 +527,33 @@ __host__ __device__ constexpr size_t grid_lds_bytes(int32_t nsph, int32_t ncells
 // loop pass, 3 now; config 2 -0.6 to -0.8%, profiles/r04/ab_variants*.txt).
 __shared__ GridDesc rtmi_grid_desc;
 __device__ __forceinline__ void stage_grid(const Accel &g) {
+  const int32_t nbs = 2 * g.nbig_pairs, nrec = nbs + g.grid.nrefs;
+  float4 *rec = rtmi_bvh_lds;
+  uint32_t *c = reinterpret_cast<uint32_t *>(rec + nrec);
+  uint16_t *ix = reinterpret_cast<uint16_t *>(c + g.grid.ncells + 1);
+  const uint32_t rec_base = lds_address(rec);
   if (threadIdx.x == 0) rtmi_grid_desc = g.grid;
-  for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) rtmi_bvh_lds[i] = g.sph[i];
-  uint32_t *c = reinterpret_cast<uint32_t *>(rtmi_bvh_lds + g.nsph);
-  uint32_t *r = c + g.grid.ncells + 1;
-  const uint32_t sph_base = lds_address(rtmi_bvh_lds), ref_base = lds_address(r);
-  for (int i = threadIdx.x; i <= g.grid.ncells; i += blockDim.x) c[i] = ref_base + 4u * g.grid.cells[i];
-  for (int i = threadIdx.x; i < g.grid.nrefs; i += blockDim.x) r[i] = sph_base + g.grid.refs[i];
+  for (int i = threadIdx.x; i < nrec; i += blockDim.x) {
+    const int32_t k = i < nbs ? g.big_idx[i] : int32_t(g.grid.refs[i - nbs] >> 4);  // dummies: -1
+    rec[i] = k < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : g.sph[k];
+    ix[i] = uint16_t(k < 0 ? 0 : k);
+  }
+  for (int i = threadIdx.x; i <= g.grid.ncells; i += blockDim.x)
+    c[i] = rec_base + 16u * (uint32_t(nbs) + g.grid.cells[i]);
   __syncthreads();
 }
 // a uint32 at an LDS address
 __device__ __forceinline__ uint32_t lds_u32(uint32_t addr) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return *(const __attribute__((address_space(3))) uint32_t *)(size_t)addr;
+#else
+  return addr;
+#endif
+}
+// a uint16 at an LDS address
+__device__ __forceinline__ uint32_t lds_u16(uint32_t addr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return *(const __attribute__((address_space(3))) uint16_t *)(size_t)addr;
 #else
   return addr;
 #endif
@@ -604,10 +622,36 @@ __device__ __forceinline__ void resolve_root(int32_t idx, float hb, float disc, 
   }
 }
 
+// resolve_root for the grid walk, whose hits are named by record-slot keys
+// (stage_grid): the same acceptance, with the scene indices read from the
+// slot index table only for an exact tie (r == t_max), which is rare, instead
+// of carried per candidate.  best_key -1: no hit yet.
+__device__ __forceinline__ void resolve_key(uint32_t key, float hb, float disc, float inv_a, float &t_max,
+                                            int32_t &best_key, uint32_t idx_base) {
+  const float sq = dsqrt(disc);
+  const float r1 = (-hb - sq) * inv_a, r2 = (-hb + sq) * inv_a;
+  const bool g1 = !(r1 < 0.001f), g2 = !(r2 < 0.001f);
+  bool ok1 = g1 & (r1 < t_max), ok2 = g2 & (r2 < t_max);
+  const bool e1 = g1 & (r1 == t_max), e2 = g2 & (r2 == t_max);
+  if (__builtin_expect(e1 | e2, 0)) {
+    const uint32_t rec_base = lds_address(rtmi_bvh_lds);
+    const uint32_t bk = best_key < 0 ? key : uint32_t(best_key);
+    const bool later = (best_key < 0) | (lds_u16(idx_base + ((key - rec_base) >> 3)) >
+                                         lds_u16(idx_base + ((bk - rec_base) >> 3)));
+    ok1 |= e1 & later;
+    ok2 |= e2 & later;
+  }
+  if (ok1 || ok2) {
+    t_max = ok1 ? r1 : r2;
+    best_key = int32_t(key);
+  }
+}
+
 // The big spheres (the ones kept out of the BVH / grid: the R = 1000 ground
 // and the r = 1 spheres) by the packed brute-force loop: group data and scene
 // indices through scalar loads, each half of a v_pk_fma_f32 an IEEE fma.
-template <int GP>
+// KEYS (the grid walk): best is a record-slot key, slot j's key rec_base + 16 j.
+template <int GP, bool KEYS = false>
 __device__ __forceinline__ void hit_big(const Accel &acc_s, V3<float> d, float K, float a, float aL, float mx, float my,
                                         float mz, float inv_a, float &t_max, int32_t &best
 #if RTMI_STATS
@@ -642,10 +686,16 @@ __device__ __forceinline__ void hit_big(const Accel &acc_s, V3<float> d, float K
 #if RTMI_STATS
       if (__lane_id() == __builtin_ctzll(__ballot(1))) stats[4] += 1;
 #endif
-      if (m & 1u) resolve_root(big_index(acc_s, 2 * q), hb0.x, d0.x, inv_a, t_max, best);
-      if (m & 2u) resolve_root(big_index(acc_s, 2 * q + 1), hb0.y, d0.y, inv_a, t_max, best);
-      if (m & 4u) resolve_root(big_index(acc_s, 2 * q + 2), hb1.x, d1.x, inv_a, t_max, best);
-      if (m & 8u) resolve_root(big_index(acc_s, 2 * q + 3), hb1.y, d1.y, inv_a, t_max, best);
+      auto res = [&](int slot, float hb, float disc) {
+        if constexpr (KEYS)  // the big slots' keys are in scene order: the plain tie rule
+          resolve_root(int32_t(lds_address(rtmi_bvh_lds) + 16u * uint32_t(slot)), hb, disc, inv_a, t_max, best);
+        else
+          resolve_root(big_index(acc_s, slot), hb, disc, inv_a, t_max, best);
+      };
+      if (m & 1u) res(2 * q, hb0.x, d0.x);
+      if (m & 2u) res(2 * q + 1, hb0.y, d0.y);
+      if (m & 4u) res(2 * q + 2, hb1.x, d1.x);
+      if (m & 8u) res(2 * q + 3, hb1.y, d1.y);
     }
   }
 }
@@ -667,7 +717,8 @@ __device__ __forceinline__ void hit_big(const Accel &acc_s, V3<float> d, float K
 // 20 x 1 x 20) — the same walk with the y axis' stepping state dropped: a y
 // face only ends the walk (5 VGPRs fewer in the loop).
 template <int GP, bool FLAT_Y = false>
-__device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> o, V3<float> d, float &t_hit
+__device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> o, V3<float> d, float &t_hit,
+                                                  uint32_t &hit_key
 #if RTMI_STATS
                                                   , unsigned *gstats
 #endif
@@ -679,13 +730,17 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
   const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
 #endif
   RTMI_RAY_TERMS(o, d)
+  // the record slots (grid_lds_bytes); the slot index table's address from
+  // the kernel arguments, a scalar (from the LDS descriptor it would be a
+  // VGPR held through the walk, which the kernel has none to spare of)
+  const uint32_t base = lds_address(rtmi_bvh_lds), idx_base = base + acc_s.grid.idx_off;
   float t_max = INFINITY;
-  int32_t best = -1;
-  hit_big<GP>(acc_s, d, K, a, aL, mx, my, mz, inv_a, t_max, best
+  int32_t best_a = -1;  // the hit's record-slot key; -1: no hit yet
+  hit_big<GP, true>(acc_s, d, K, a, aL, mx, my, mz, inv_a, t_max, best_a
 #if RTMI_STATS
               , gstats
 #endif
-  );
+              );
 #if RTMI_TRACE_PHASES
   const unsigned long long tp1 = __builtin_amdgcn_s_memtime();
   pc.c[0] += tp1 - tp0;
@@ -703,8 +758,7 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
   const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(bx0, bx1), __builtin_fmaxf(by0, by1)),
                                      __builtin_fminf(__builtin_fmaxf(bz0, bz1), t_max));
   if (tnear <= tfar) {
-    const uint32_t base = lds_address(rtmi_bvh_lds);
-    const uint32_t cells = lds_address(rtmi_bvh_lds + acc_s.nsph);  // LDS address of cell 0's start
+    const uint32_t cells = base + G.cells_off;
     // entry cell: the cell of o + tnear*d, clamped into the grid
     auto cell_of = [&](float p, int ax) {
       const int c = int(__builtin_floorf((p - G.g0[ax]) * G.inv_h[ax]));
@@ -745,10 +799,6 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
 #if RTMI_TRACE_PHASES
     tp2 = __builtin_amdgcn_s_memtime();
 #endif
-    // The tie rule compares scene indices; in the walk it compares the
-    // spheres' LDS addresses instead (base + 16 x scene index: the same
-    // order), so no index is computed per resolution.  -1: no hit yet.
-    int32_t best_a = best < 0 ? -1 : int32_t(base + 16u * uint32_t(best));
     for (;;) {
 #if RTMI_STATS
       gstats[0] += 1;
@@ -763,25 +813,24 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
       // The result is the same: resolve_root's acceptance is order-independent
       // (the closest root, ties to the larger index), and the walk's exit
       // test comes after the cell's resolutions either way.  (0: none; every
-      // sphere address is above the kernel's static LDS.)
+      // slot address is above the kernel's static LDS.)
       uint32_t kaddr = 0u;
       float khb = 0.0f, kdisc = 0.0f;
-      for (uint32_t r = lds_u32(cell); r < re; r += 4u) {
+      for (uint32_t r = lds_u32(cell); r < re; r += 16u) {
 #if RTMI_STATS
         gstats[1] += 1;
         if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[3] += 1;
 #endif
-        const uint32_t addr = lds_u32(r);
         float hb, disc;
-        sphere_test(lds_sphere(addr), d, K, a, aL, mx, my, mz, hb, disc);
+        sphere_test(lds_sphere(r), d, K, a, aL, mx, my, mz, hb, disc);
         if (!(disc < 0.0f)) {
           if (kaddr != 0u) {
 #if RTMI_STATS
             if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
 #endif
-            resolve_root(int32_t(kaddr), khb, kdisc, inv_a, t_max, best_a);
+            resolve_key(kaddr, khb, kdisc, inv_a, t_max, best_a, idx_base);
           }
-          kaddr = addr;
+          kaddr = r;
           khb = hb;
           kdisc = disc;
         }
@@ -790,7 +839,7 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
 #if RTMI_STATS
         if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
 #endif
-        resolve_root(int32_t(kaddr), khb, kdisc, inv_a, t_max, best_a);
+        resolve_key(kaddr, khb, kdisc, inv_a, t_max, best_a, idx_base);
       }
       const float texit = __builtin_fminf(tnx, __builtin_fminf(tny, tnz));
       if constexpr (FLAT_Y) {
@@ -826,7 +875,6 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
         cell += dcz;
       }
     }
-    best = best_a < 0 ? -1 : int32_t((uint32_t(best_a) - base) >> 4);
   }
 #if RTMI_TRACE_PHASES
   {
@@ -836,7 +884,10 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
   }
 #endif
   t_hit = t_max;
-  return best;
+  // the scene index of the hit slot (a miss reads slot 0's, unused)
+  hit_key = best_a < 0 ? base : uint32_t(best_a);
+  const int32_t k = int32_t(lds_u16(idx_base + ((hit_key - base) >> 3)));
+  return best_a < 0 ? -1 : k;
 }
 
 template <int GP>

@@ -362,7 +362,9 @@ def test_bvh_bit_exact_vs_oracle_final(kernel, accel, final_world, final_rendere
     nb, nn = final_renderer.accel_info()
     assert nb == 4 and nn > 100  # ground + the three r=1 spheres stay brute force
     dims, nrefs, lds = final_renderer.grid_info()
-    assert dims[1] == 1 and dims[0] * dims[2] >= 400 and nrefs >= 483 and lds <= 20480, (dims, nrefs, lds)
+    # the record slots + 1.5 KB of shared accumulators + ~0.2 KB of static LDS
+    # must stay within 20 KB per 4-wave block: 8 blocks per CU
+    assert dims[1] == 1 and dims[0] * dims[2] >= 400 and nrefs >= 483 and lds + 1536 + 256 <= 20480, (dims, nrefs, lds)
     final_renderer.set_accel(accel)
     final_renderer.set_kernel(kernel)
     try:

@@ -116,6 +116,21 @@ def launch(args, argv):
     return subprocess.call(cmd)
 
 
+def init_group(dist, backend, **kw):
+    """init_process_group with the process's fd 1 pointed at fd 2 meanwhile:
+    a backend's own start-up chatter (gloo prints its peer connections to
+    stdout from C++) must not reach stdout, which carries only the JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        dist.init_process_group(backend, **kw)
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def dist_setup(torch, dist):
     """One process per GPU (torch.distributed.run env).  RCCL ("nccl") is the
     product path.  RTMI_DIST_BACKEND=gloo is a rehearsal mode for a box with
@@ -130,7 +145,7 @@ def dist_setup(torch, dist):
         if backend != "gloo":
             raise SystemExit("bench: RTMI_BENCH_STUB=1 needs RTMI_DIST_BACKEND=gloo")
         if world_size > 1:
-            dist.init_process_group("gloo")
+            init_group(dist, "gloo")
         cpu = torch.device("cpu")
         return world_size, rank, -1, cpu, cpu
     ndev = torch.cuda.device_count()
@@ -141,9 +156,9 @@ def dist_setup(torch, dist):
     dev = torch.device("cuda", device)
     if world_size > 1:
         if backend == "gloo":
-            dist.init_process_group("gloo")
+            init_group(dist, "gloo")
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            init_group(dist, "nccl", device_id=dev)
     coll = dev if backend == "nccl" else torch.device("cpu")
     return world_size, rank, device, dev, coll
 

@@ -24,8 +24,10 @@ def test_bench_n_ranks_line_schema(n, tmp_path):
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--steps", "2", "--warmup", "1"],
                        capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
     assert p.returncode == 0, p.stderr[-3000:]
-    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, p.stdout[-2000:]  # rank 0 prints ONE line
+    lines = p.stdout.splitlines()
+    # rank 0 prints ONE line and nothing else reaches stdout (gloo's start-up
+    # chatter included: bench.init_group)
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["stub"] is True and d["data"].startswith("STUB")
     assert d["n_gpus"] == n and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "strong"

@@ -1294,9 +1294,13 @@ bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, int32_t 
     vol *= e[a];
   }
   const double cell = std::cbrt(vol / (per_sphere * double(small.size())));
+  // analysis knob: RTMI_GRID_ASPECT = x-cell / z-cell size ratio (1: cubic)
+  const char *asp_env = std::getenv("RTMI_GRID_ASPECT");
+  const double asp = asp_env && std::atof(asp_env) > 0 ? std::atof(asp_env) : 1.0;
+  const double cell_a[3] = {cell * std::sqrt(asp), cell, cell / std::sqrt(asp)};
   int64_t total = 1;
   for (int a = 0; a < 3; ++a) {
-    out.desc.n[a] = int32_t(std::min<double>(128, std::max<double>(1, std::ceil(e[a] / cell))));
+    out.desc.n[a] = int32_t(std::min<double>(128, std::max<double>(1, std::ceil(e[a] / cell_a[a]))));
     total *= out.desc.n[a];
   }
   if (total > 16384) return false;

@@ -17,9 +17,22 @@
 //
 // bench.py's multi-GPU path is the one-process-per-GPU equivalent
 // (torch.distributed over RCCL); this entry point serves C/C++ callers.
+//
+// Mock gather (analysis and tests only): with
+// RTMI_MULTI_MOCK=1 in the environment at rt_multi_create, logical device g
+// runs on physical device g % visible (each logical device its own context and
+// stream, so G logical devices can share one GPU) and the gather is a
+// peer copy of each strip into device 0's receive buffer on device 0's stream
+// after that strip's end event, in place of ncclCommInitAll / ncclGather.
+// Everything else is the product's code: streams, events, drains, progressive
+// passes, rt_unpermute_rows.  With the mock, RTMI_MULTI_MOCK_FAIL=g (read per
+// call) makes rt_multi_render / _render_pass / _accum_resolve fail on logical
+// device g after devices 0..g-1 have enqueued their work: the partial-failure
+// path the drains exist for.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -44,22 +57,25 @@ struct rt_multi {
   std::vector<float> strip_ms;
   float gather_ms = -1.0f;
   int32_t pass_W = 0, pass_H = 0, pass_nrows = 0;  // progressive accumulators (0: none)
+  int visible = 1;    // physical devices
+  bool mock = false;  // RTMI_MULTI_MOCK: logical devices over the visible ones, copy gather
+  int dev(int g) const { return mock ? g % visible : g; }  // logical -> physical device
 };
 
 namespace {
 void destroy(rt_multi *m) {
   if (!m) return;
   for (int g = 0; g < int(m->ctx.size()); g++)
-    if (m->ctx[g]) { (void)hipSetDevice(g); (void)rt_ctx_synchronize(m->ctx[g]); }
+    if (m->ctx[g]) { (void)hipSetDevice(m->dev(g)); (void)rt_ctx_synchronize(m->ctx[g]); }
   for (auto c : m->comm)
     if (c) ncclCommDestroy(c);
   for (size_t g = 0; g < m->strip.size(); g++) {
-    (void)hipSetDevice(int(g));
+    (void)hipSetDevice(m->dev(int(g)));
     if (m->strip[g]) (void)hipFree(m->strip[g]);
     if (g < m->ev_begin.size() && m->ev_begin[g]) (void)hipEventDestroy(m->ev_begin[g]);
     if (g < m->ev_end.size() && m->ev_end[g]) (void)hipEventDestroy(m->ev_end[g]);
   }
-  (void)hipSetDevice(0);
+  (void)hipSetDevice(m->dev(0));
   if (m->recv) (void)hipFree(m->recv);
   if (m->gather_begin) (void)hipEventDestroy(m->gather_begin);
   if (m->gather_end) (void)hipEventDestroy(m->gather_end);
@@ -75,7 +91,7 @@ void destroy(rt_multi *m) {
 int drain(rt_multi *m, int rc) {
   for (int g = 0; g < int(m->ctx.size()); g++)
     if (m->ctx[g]) {
-      (void)hipSetDevice(g);
+      (void)hipSetDevice(m->dev(g));
       (void)hipStreamSynchronize(rtmi::ctx_stream(m->ctx[g]));
     }
   return rc;
@@ -91,7 +107,7 @@ struct KeepDevice {
 int ensure_buffers(rt_multi *m, size_t strip_elems) {
   if (strip_elems > m->strip_cap) {
     for (int g = 0; g < m->G; g++) {
-      (void)hipSetDevice(g);
+      (void)hipSetDevice(m->dev(g));
       if (m->strip[g]) (void)hipFree(m->strip[g]);
       m->strip[g] = nullptr;
       if (hipMalloc(&m->strip[g], strip_elems * sizeof(float)) != hipSuccess) {
@@ -102,7 +118,7 @@ int ensure_buffers(rt_multi *m, size_t strip_elems) {
     m->strip_cap = strip_elems;
   }
   if (strip_elems * m->G > m->recv_cap) {
-    (void)hipSetDevice(0);
+    (void)hipSetDevice(m->dev(0));
     if (m->recv) (void)hipFree(m->recv);
     m->recv = nullptr;
     if (hipMalloc(&m->recv, strip_elems * m->G * sizeof(float)) != hipSuccess) {
@@ -114,6 +130,25 @@ int ensure_buffers(rt_multi *m, size_t strip_elems) {
   return RT_OK;
 }
 
+// RTMI_MULTI_MOCK_FAIL=g: the injected failure of logical device g (mock only)
+int injected_failure(const rt_multi *m, int g, const char *what) {
+  if (!m->mock) return RT_OK;
+  const char *f = std::getenv("RTMI_MULTI_MOCK_FAIL");
+  if (f && *f && std::atoi(f) == g) return set_error(RT_EHIP, "%s: injected failure on logical device %d (RTMI_MULTI_MOCK_FAIL)", what, g);
+  return RT_OK;
+}
+
+// The mock's exchange step: each strip copied into device 0's receive buffer
+// on device 0's stream, in rank order, after device 0 has waited for every
+// strip (gather_unpermute_body) — what ncclGather does, with no communicator.
+int mock_gather(rt_multi *m, size_t strip_elems, hipStream_t s0) {
+  for (int g = 0; g < m->G; g++)
+    if (hipMemcpyPeerAsync(m->recv + size_t(g) * strip_elems, m->dev(0), m->strip[g], m->dev(g),
+                           strip_elems * sizeof(float), s0) != hipSuccess)
+      return set_error(RT_EHIP, "mock gather copy of strip %d", g);
+  return RT_OK;
+}
+
 // The single exchange step: every strip (already enqueued on its device's
 // stream) to GPU 0, then rows un-permuted into the host image.
 int gather_unpermute_body(rt_multi *m, int32_t W, int32_t H, int32_t nrows, float *sum) {
@@ -122,34 +157,39 @@ int gather_unpermute_body(rt_multi *m, int32_t W, int32_t H, int32_t nrows, floa
   std::vector<hipStream_t> streams(G);
   for (int g = 0; g < G; g++) streams[g] = rtmi::ctx_stream(m->ctx[g]);
   // device 0 starts the gather clock once every strip is rendered
-  (void)hipSetDevice(0);
+  (void)hipSetDevice(m->dev(0));
   for (int g = 1; g < G; g++)
     if (hipStreamWaitEvent(streams[0], m->ev_end[g], 0) != hipSuccess) return set_error(RT_EHIP, "wait for GPU %d", g);
   if (hipEventRecord(m->gather_begin, streams[0]) != hipSuccess) return set_error(RT_EHIP, "gather event");
-  ncclResult_t r = ncclGroupStart();
-  for (int g = 0; g < G && r == ncclSuccess; g++) {
-    (void)hipSetDevice(g);
-    r = ncclGather(m->strip[g], g == 0 ? m->recv : nullptr, strip_elems, ncclFloat, 0, m->comm[g], streams[g]);
+  if (m->mock) {
+    if (int rc = mock_gather(m, strip_elems, streams[0])) return rc;
+  } else {
+    ncclResult_t r = ncclGroupStart();
+    for (int g = 0; g < G && r == ncclSuccess; g++) {
+      (void)hipSetDevice(g);
+      r = ncclGather(m->strip[g], g == 0 ? m->recv : nullptr, strip_elems, ncclFloat, 0, m->comm[g], streams[g]);
+    }
+    ncclResult_t r2 = ncclGroupEnd();
+    if (r == ncclSuccess) r = r2;
+    if (r != ncclSuccess) return set_error(RT_ERCCL, "ncclGather: %s", ncclGetErrorString(r));
   }
-  ncclResult_t r2 = ncclGroupEnd();
-  if (r == ncclSuccess) r = r2;
-  if (r != ncclSuccess) return set_error(RT_ERCCL, "ncclGather: %s", ncclGetErrorString(r));
-  (void)hipSetDevice(0);
+  (void)hipSetDevice(m->dev(0));
   if (hipEventRecord(m->gather_end, streams[0]) != hipSuccess) return set_error(RT_EHIP, "gather event");
   for (int g = 0; g < G; g++) {
-    (void)hipSetDevice(g);
+    (void)hipSetDevice(m->dev(g));
     if (hipStreamSynchronize(streams[g]) != hipSuccess) return set_error(RT_EHIP, "sync GPU %d", g);
+    if (m->mock) continue;
     ncclResult_t ae = ncclSuccess;
     ncclCommGetAsyncError(m->comm[g], &ae);
     if (ae != ncclSuccess) return set_error(RT_ERCCL, "RCCL async error on GPU %d: %s", g, ncclGetErrorString(ae));
   }
   m->strip_ms.assign(G, -1.0f);
   for (int g = 0; g < G; g++) {
-    (void)hipSetDevice(g);
+    (void)hipSetDevice(m->dev(g));
     float ms = -1.0f;
     if (hipEventElapsedTime(&ms, m->ev_begin[g], m->ev_end[g]) == hipSuccess) m->strip_ms[g] = ms;
   }
-  (void)hipSetDevice(0);
+  (void)hipSetDevice(m->dev(0));
   if (hipEventElapsedTime(&m->gather_ms, m->gather_begin, m->gather_end) != hipSuccess) m->gather_ms = -1.0f;
   m->host.resize(strip_elems * G);
   if (hipMemcpy(m->host.data(), m->recv, m->host.size() * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
@@ -168,28 +208,32 @@ RTMI_EXPORT int rt_multi_create(const rt_scene *scene, int32_t n_gpus, rt_multi 
   if (!scene || n_gpus < 0) return set_error(RT_EINVAL, "rt_multi_create: bad argument");
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return set_error(RT_ENODEVICE, "no HIP device visible");
+  const char *mk = std::getenv("RTMI_MULTI_MOCK");
+  const bool mock = mk && *mk && *mk != '0';
   const int G = n_gpus == 0 ? count : n_gpus;
-  if (G > count) return set_error(RT_ENODEVICE, "asked for %d GPUs, %d visible", G, count);
+  if (G > count && !mock) return set_error(RT_ENODEVICE, "asked for %d GPUs, %d visible", G, count);
   KeepDevice keep;
   rt_multi *m = new rt_multi;
   m->G = G;
+  m->visible = count;
+  m->mock = mock;
   m->ctx.assign(G, nullptr);
   m->strip.assign(G, nullptr);
   m->ev_begin.assign(G, nullptr);
   m->ev_end.assign(G, nullptr);
   int rc = RT_OK;
   for (int g = 0; g < G && rc == RT_OK; g++) {
-    if ((rc = rt_ctx_create(g, &m->ctx[g])) || (rc = rt_ctx_set_scene(m->ctx[g], scene))) break;
-    (void)hipSetDevice(g);
+    if ((rc = rt_ctx_create(m->dev(g), &m->ctx[g])) || (rc = rt_ctx_set_scene(m->ctx[g], scene))) break;
+    (void)hipSetDevice(m->dev(g));
     if (hipEventCreate(&m->ev_begin[g]) != hipSuccess || hipEventCreate(&m->ev_end[g]) != hipSuccess)
       rc = set_error(RT_EHIP, "events on GPU %d", g);
   }
   if (rc == RT_OK) {
-    (void)hipSetDevice(0);
+    (void)hipSetDevice(m->dev(0));
     if (hipEventCreate(&m->gather_begin) != hipSuccess || hipEventCreate(&m->gather_end) != hipSuccess)
       rc = set_error(RT_EHIP, "gather events");
   }
-  if (rc == RT_OK) {
+  if (rc == RT_OK && !mock) {
     m->comm.assign(G, nullptr);
     std::vector<int> devs(G);
     for (int g = 0; g < G; g++) devs[g] = g;
@@ -234,11 +278,12 @@ RTMI_EXPORT int rt_multi_render(rt_multi *m, const rt_camera *cam, int32_t W, in
   int rc = ensure_buffers(m, size_t(nrows) * W * 3);
   // every strip enqueued on its own device's stream, then the gather
   for (int g = 0; g < G && rc == RT_OK; g++) {
-    (void)hipSetDevice(g);
+    (void)hipSetDevice(m->dev(g));
     hipStream_t s = rtmi::ctx_stream(m->ctx[g]);
     if (hipEventRecord(m->ev_begin[g], s) != hipSuccess) rc = set_error(RT_EHIP, "event on GPU %d", g);
+    if (rc == RT_OK) rc = injected_failure(m, g, "rt_multi_render");
     if (rc == RT_OK) rc = rt_render_rows(m->ctx[g], cam, W, H, spp, max_depth, seed, g, G, nrows, m->strip[g], nullptr);
-    (void)hipSetDevice(g);
+    (void)hipSetDevice(m->dev(g));
     if (rc == RT_OK && hipEventRecord(m->ev_end[g], s) != hipSuccess) rc = set_error(RT_EHIP, "event on GPU %d", g);
   }
   if (rc != RT_OK) return drain(m, rc);  // earlier devices' strips may be in flight
@@ -273,13 +318,14 @@ RTMI_EXPORT int rt_multi_render_pass(rt_multi *m, const rt_camera *cam, int32_t 
   KeepDevice keep;
   int rc = RT_OK;
   for (int g = 0; g < m->G && rc == RT_OK; g++) {
-    (void)hipSetDevice(g);
+    (void)hipSetDevice(m->dev(g));
     hipStream_t s = rtmi::ctx_stream(m->ctx[g]);
     if (hipEventRecord(m->ev_begin[g], s) != hipSuccess) rc = set_error(RT_EHIP, "event on GPU %d", g);
+    if (rc == RT_OK) rc = injected_failure(m, g, "rt_multi_render_pass");
     if (rc == RT_OK)
       rc = rt_render_pass(m->ctx[g], cam, m->pass_W, m->pass_H, s_begin, s_count, max_depth, seed, g, m->G,
                           m->pass_nrows, nullptr);
-    (void)hipSetDevice(g);
+    (void)hipSetDevice(m->dev(g));
     if (rc == RT_OK && hipEventRecord(m->ev_end[g], s) != hipSuccess) rc = set_error(RT_EHIP, "event on GPU %d", g);
   }
   if (rc != RT_OK) {
@@ -298,11 +344,12 @@ RTMI_EXPORT int rt_multi_accum_resolve(rt_multi *m, float *sum) {
   KeepDevice keep;
   int rc = ensure_buffers(m, size_t(m->pass_nrows) * m->pass_W * 3);
   for (int g = 0; g < m->G && rc == RT_OK; g++) {
-    (void)hipSetDevice(g);
+    (void)hipSetDevice(m->dev(g));
     hipStream_t s = rtmi::ctx_stream(m->ctx[g]);
     if (hipEventRecord(m->ev_begin[g], s) != hipSuccess) rc = set_error(RT_EHIP, "event on GPU %d", g);
+    if (rc == RT_OK) rc = injected_failure(m, g, "rt_multi_accum_resolve");
     if (rc == RT_OK) rc = rt_accum_resolve(m->ctx[g], m->strip[g], nullptr, nullptr);
-    (void)hipSetDevice(g);
+    (void)hipSetDevice(m->dev(g));
     if (rc == RT_OK && hipEventRecord(m->ev_end[g], s) != hipSuccess) rc = set_error(RT_EHIP, "event on GPU %d", g);
   }
   if (rc != RT_OK) return drain(m, rc);

@@ -812,9 +812,11 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
       // candidate (tools/grid_sim.c: 3.4 instead of 4.8 per wave-segment).
       // The result is the same: resolve_root's acceptance is order-independent
       // (the closest root, ties to the larger index), and the walk's exit
-      // test comes after the cell's resolutions either way.  (0: none; every
-      // slot address is above the kernel's static LDS.)
-      uint32_t kaddr = 0u;
+      // test comes after the cell's resolutions either way.  (kNoKey: none —
+      // an explicit sentinel no LDS address can take, not 0, which slot 0
+      // would be if nothing preceded the dynamic LDS)
+      constexpr uint32_t kNoKey = 0xFFFFFFFFu;
+      uint32_t kaddr = kNoKey;
       float khb = 0.0f, kdisc = 0.0f;
       for (uint32_t r = lds_u32(cell); r < re; r += 16u) {
 #if RTMI_STATS
@@ -824,7 +826,7 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
         float hb, disc;
         sphere_test(lds_sphere(r), d, K, a, aL, mx, my, mz, hb, disc);
         if (!(disc < 0.0f)) {
-          if (kaddr != 0u) {
+          if (kaddr != kNoKey) {
 #if RTMI_STATS
             if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
 #endif
@@ -835,7 +837,7 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
           kdisc = disc;
         }
       }
-      if (kaddr != 0u) {
+      if (kaddr != kNoKey) {
 #if RTMI_STATS
         if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
 #endif

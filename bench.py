@@ -116,15 +116,42 @@ def launch(args, argv):
     return subprocess.call(cmd)
 
 
+# Collective timeout (s) of the process group: a rank that stalls (a hung
+# first RCCL gather, a dead peer) ends the run within this bound instead of
+# torch's default 10 minutes.  It covers rank 0's untimed side renders while
+# the other ranks wait at a barrier (the whole-frame gather check: 0.7 s at
+# config 5 on one GPU) and RCCL's communicator set-up in the first collective.
+# RTMI_DIST_TIMEOUT_S overrides it (tests use a few seconds).
+DIST_TIMEOUT_S = float(os.environ.get("RTMI_DIST_TIMEOUT_S", "60"))
+
+
+class CollectiveError(RuntimeError):
+    """A collective of the process group failed or timed out on this rank."""
+
+
+def collective(name, fn, *a, **kw):
+    """Run one torch.distributed call; a failure (gloo: a timeout raises here;
+    RCCL: torch's watchdog aborts the process and names the work itself)
+    becomes a CollectiveError naming the collective."""
+    try:
+        return fn(*a, **kw)
+    except Exception as e:
+        raise CollectiveError(f"{name}: {type(e).__name__}: {str(e).splitlines()[0] if str(e) else ''}") from e
+
+
 def init_group(dist, backend, **kw):
     """init_process_group with the process's fd 1 pointed at fd 2 meanwhile:
     a backend's own start-up chatter (gloo prints its peer connections to
-    stdout from C++) must not reach stdout, which carries only the JSON line."""
+    stdout from C++) must not reach stdout, which carries only the JSON line.
+    Every collective of the group times out after DIST_TIMEOUT_S."""
+    from datetime import timedelta
+
     sys.stdout.flush()
     saved = os.dup(1)
     try:
         os.dup2(2, 1)
-        dist.init_process_group(backend, **kw)
+        collective("init_process_group", dist.init_process_group, backend,
+                   timeout=timedelta(seconds=DIST_TIMEOUT_S), **kw)
     finally:
         sys.stdout.flush()
         os.dup2(saved, 1)
@@ -170,6 +197,10 @@ def dist_setup(torch, dist):
 # by tests/test_bench_dist.py to rehearse N > 1 where no GPU exists; the line
 # it prints is marked "stub" and is never a measurement.
 STUB = os.environ.get("RTMI_BENCH_STUB") == "1"
+# tests/test_bench_dist.py only (stub runs): rank RTMI_BENCH_STALL_RANK sleeps
+# RTMI_BENCH_STALL_S seconds before each gather, past the collective timeout
+STALL_RANK = int(os.environ.get("RTMI_BENCH_STALL_RANK", "-1")) if STUB else -1
+STALL_S = float(os.environ.get("RTMI_BENCH_STALL_S", "0"))
 
 
 class StubRenderer:
@@ -551,8 +582,8 @@ def main():
 
     def collect(b):
         nonlocal gathered
-        _, bufs, work, _src = pend.pop(b)
-        work.wait()
+        k, bufs, work, _src = pend.pop(b)
+        collective(f"gather of step {k}'s strips (wait)", work.wait)
         gathered = bufs
 
     def step(record):
@@ -565,9 +596,12 @@ def main():
             ev.append(timed_render(buf=buf))
         else:
             render_into((row0, row_step, nrows), buf)
+        if STALL_RANK == rank:  # test only: this rank stalls before its gather
+            time.sleep(STALL_S)
         if N > 1:  # the single exchange step: strips -> rank 0 over RCCL/xGMI, overlapping the next render
             src = buf if coll.type == dev.type else buf.cpu()  # (gloo rehearsal: host copy)
-            bufs, work = rdist.gather_strips(src, rank, N, dst=0, async_op=True)
+            bufs, work = collective(f"gather of step {nstep[0]}'s strips", rdist.gather_strips, src, rank, N, dst=0,
+                                    async_op=True)
             pend[b] = (nstep[0], bufs, work, src)  # the source stays referenced until the gather is done
 
     def drain():  # every gather in flight, in the order issued (the last one's strips are `gathered`)
@@ -579,7 +613,7 @@ def main():
     drain()
     sync()
     if N > 1:
-        dist.barrier()
+        collective("barrier before the timed region", dist.barrier)
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -587,12 +621,12 @@ def main():
     drain()
     sync()
     if N > 1:
-        dist.barrier()
+        collective("barrier after the timed region", dist.barrier)
     sync()
     elapsed = my_elapsed = time.perf_counter() - t0
     if N > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        collective("all_reduce(max) of the timed region", dist.all_reduce, t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
@@ -606,7 +640,8 @@ def main():
         render_into((row0, row_step, nrows), strip)
         g0, g1 = Event(enable_timing=True), Event(enable_timing=True)
         g0.record(stream)
-        rdist.gather_strips(strip if coll.type == dev.type else strip.cpu(), rank, N, dst=0)
+        collective("blocking gather (gather_ms)", rdist.gather_strips,
+                   strip if coll.type == dev.type else strip.cpu(), rank, N, dst=0)
         g1.record(stream)
         sync()
         gev.append((g0, g1))
@@ -616,7 +651,7 @@ def main():
         gather_ms = float(np.mean([a.elapsed_time(b) for a, b in gev]))
         mine = torch.tensor([kernel_ms, gather_ms, float(segs), my_elapsed], dtype=torch.float64, device=coll)
         every = [torch.zeros_like(mine) for _ in range(N)]
-        dist.all_gather(every, mine)
+        collective("all_gather of per-rank timings", dist.all_gather, every, mine)
         every = np.array([e.cpu().numpy() for e in every])
         total_segs = float(every[:, 2].sum())
         kernel_ms_max = float(every[:, 0].max())
@@ -648,7 +683,7 @@ def main():
                             "one_gpu_frame_ms": round(e0.elapsed_time(e1), 3)}
             if not equal:
                 print(f"bench: gathered {N}-GPU image differs from the 1-GPU frame: {gather_check}", file=sys.stderr)
-        dist.barrier()
+        collective("barrier after the gather check", dist.barrier)
 
     # one-shot render (the reference's use case renders once, main.cpp:292-360):
     # no cost map from a previous identical render, so the library runs its
@@ -897,25 +932,26 @@ def bench_nw(args):
             e1.record(stream)
             ev.append((e0, e1))
         if N > 1:
-            rdist.gather_strips(strip if coll.type == "cuda" else strip.cpu(), rank, N, dst=0)
+            collective("gather of the strips", rdist.gather_strips, strip if coll.type == "cuda" else strip.cpu(), rank, N,
+                       dst=0)
 
     for _ in range(args.warmup):
         step(False)
     torch.cuda.synchronize(dev)
     if N > 1:
-        dist.barrier()
+        collective("barrier before the timed region", dist.barrier)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
     torch.cuda.synchronize(dev)
     if N > 1:
-        dist.barrier()
+        collective("barrier after the timed region", dist.barrier)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if N > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        collective("all_reduce(max) of the timed region", dist.all_reduce, t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     segs = r.last_segments()
@@ -978,4 +1014,13 @@ def bench_nw(args):
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except CollectiveError as e:
+        # a stalled or failed collective: non-zero at once, rank and collective
+        # on stderr, stdout untouched (the JSON line is printed only at the
+        # end); os._exit, since tearing down a group whose peer is stuck can
+        # block (the reference's check_cuda exits the process too, final.cu:13-24)
+        print(f"bench: rank {os.environ.get('RANK', '0')} of {os.environ.get('WORLD_SIZE', '1')}: collective failed "
+              f"(timeout {DIST_TIMEOUT_S:g} s): {e}", file=sys.stderr, flush=True)
+        os._exit(5)

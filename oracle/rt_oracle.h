@@ -99,11 +99,11 @@ void or_fast_rng(uint64_t seed, uint64_t pixel, uint32_t sample, int32_t n, uint
 /* n draws of the fast-mode direct samplers (kind 0 unit direction, 1 unit
  * ball, 2 unit disk; 3 sincos2pi on a v grid) as xyz triples. */
 void or_fast_dirs(int32_t kind, uint64_t seed, int32_t n, float *out);
-/* Total path segments (world.hit calls) of the fast-mode render, for the
- * algorithmic-work accounting of bench.py (DESIGN.md §5). */
 /* Largest ulp distance between (i + r) * (1/D) and (i + r) / D over every
  * float numerator the fast mode forms (i in [0, D], r a 24-bit uniform). */
 int32_t or_uv_forms(int32_t D, int64_t *n_checked, int64_t *n_diff);
+/* Total path segments (world.hit calls) of the fast-mode render, for the
+ * algorithmic-work accounting of bench.py (DESIGN.md §5). */
 int64_t or_fast_segments(const or_scene *s, const or_camera *c, int32_t W, int32_t H,
                          int32_t spp, int32_t max_depth, uint64_t seed, int32_t row0,
                          int32_t row_step, int32_t nrows);

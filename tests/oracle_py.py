@@ -278,3 +278,22 @@ def nw_trace(flat, nwcam, W, H, depth, seed, i, j, smp, cap=64):
                       rec.ctypes.data_as(_fp), cap)
     out = rec[: 12 * n].reshape(-1, 12).copy()
     return out[:, [0, 1, 2, 3, 4, 5, 6, 8, 9, 10]], out[:, [7, 11]].view(np.int32)
+
+
+def row_mean_z(frame_rows, S, a, b, s_ab):
+    """Per-row, per-channel z-scores of a frame's row means against two
+    independent oracle renders of the same rows (sums at s_ab spp under two
+    other seeds), and the mean of z^2 (chi-square per degree of freedom).
+    The noise of a row mean is measured, not assumed: the per-pixel
+    difference of the two oracle renders has variance 2 s^2 / s_ab per pixel
+    (s^2 the per-sample variance), pooled over the row's pixels; the frame's
+    own noise (S spp) is added at the same per-sample variance."""
+    f = np.asarray(frame_rows, np.float64) / S
+    ma, mb = np.asarray(a, np.float64) / s_ab, np.asarray(b, np.float64) / s_ab
+    W = f.shape[1]
+    var1 = s_ab * ((ma - mb) ** 2).mean(axis=1) / 2.0  # per-sample variance, per row and channel
+    var_ref = var1 / (2 * s_ab * W)  # the mean of the two oracle renders' row means
+    var_frame = var1 / (S * W)
+    d = f.mean(axis=1) - (ma + mb).mean(axis=1) / 2.0
+    z = d / np.sqrt(var_ref + var_frame + 1e-30)
+    return z, float((z ** 2).mean())

@@ -53,3 +53,25 @@ def test_stub_requires_gloo():
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "1"], capture_output=True, text=True,
                        timeout=300, env=env)
     assert p.returncode != 0 and "needs RTMI_DIST_BACKEND=gloo" in p.stderr
+
+
+def test_stalled_rank_fails_fast_with_rank_and_collective_named(tmp_path):
+    """a rank that stalls past the collective timeout
+    (here rank 1 sleeps 120 s before its first gather, the timeout is 4 s)
+    ends the whole run non-zero well inside the stall, with the failing rank
+    and the collective named on stderr and nothing on stdout (no partial
+    line).  Replaces the reference's error behaviour, check_cuda's exit(99)
+    (accelerated-rt-cuda/final.cu:13-24)."""
+    import time
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(RTMI_DIST_BACKEND="gloo", RTMI_BENCH_STUB="1", OMP_NUM_THREADS="1", RTMI_DIST_TIMEOUT_S="4",
+               RTMI_BENCH_STALL_RANK="1", RTMI_BENCH_STALL_S="120")
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=110, env=env, cwd=str(tmp_path))
+    took = time.monotonic() - t0
+    assert p.returncode != 0
+    assert took < 100, took  # not the stall's 120 s, nor torch's 10-minute default
+    assert p.stdout.strip() == "", p.stdout[-2000:]
+    assert "bench: rank 0 of 2: collective failed (timeout 4 s): gather of step 1's strips" in p.stderr, p.stderr[-3000:]

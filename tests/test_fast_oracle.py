@@ -8,6 +8,7 @@ the reference statistically: same mean path length (world.hit calls per
 sample) and same mean radiance as the ref-mode restatement, which is itself
 bit-exact against the reference (test_oracle_golden.py)."""
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -135,3 +136,25 @@ def test_fixed_point_guard_non_finite_colours():
     assert np.isfinite(out).all()
     assert out.max() == 64.0 * 8  # a pixel whose 8 samples all saturate
     assert out.min() >= 0.0
+
+
+def test_row_mean_z_statistic_on_oracle_renders():
+    """The config-5 row-mean check's statistic (O.row_mean_z) on the CPU:
+    an oracle render of 2 config-5-wide rows at 128 spp against two other
+    seeds at 32 spp sits within its noise; the same frame with one row's
+    brightness off by 1.5% is flagged."""
+    import numpy as np
+
+    world = O.load_scene_txt(os.path.join(O.GOLDEN, "scene_final.txt"))
+    W, H = 3840, 2160
+    cam = O.final_camera(W / H)
+    rows = dict(row0=200, row_step=1300, nrows=2)
+    f = O.fast_render(world, cam, W, H, 128, 50, 1984, **rows)
+    a = O.fast_render(world, cam, W, H, 32, 50, 7, **rows)
+    b = O.fast_render(world, cam, W, H, 32, 50, 8, **rows)
+    z, chi2 = O.row_mean_z(f, 128, a, b, 32)
+    assert z.shape == (2, 3) and np.abs(z).max() < 5.0 and chi2 < 6.0, z
+    f2 = f.copy()
+    f2[1] *= 1.015
+    z2, _ = O.row_mean_z(f2, 128, a, b, 32)
+    assert np.abs(z2[1]).max() > 5.0, z2

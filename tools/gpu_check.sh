@@ -1,15 +1,18 @@
 #!/bin/bash
-# Round 4: the driver's round-end commands on the current tree (GPU suite,
-# smoke, default bench line), then optional extra steps:
+# The driver's round-end commands on the current tree (GPU suite, smoke,
+# default bench line), then optional extra steps:
+#   TESTS="<pytest args>"  run only these GPU tests (default: tests -m gpu)
 #   OLDLIB=<name>  the adversarial-ray tests against lib/librtmi_<name>.so
 #                  (a build of an older tree: shows what a fix changed)
 #   STRIP=1        the 1/8 strip line
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-OUT=gpurun_out/${TAG:-r04_check}
+OUT=gpurun_out/${TAG:-check}
 mkdir -p $OUT
-timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
+rm -f gpurun_out/parity_stats.json
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
+cp gpurun_out/parity_stats.json $OUT/ 2>/dev/null
 tail -1 $OUT/pytest_gpu.log
 timeout -k 10 240 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
 tail -1 $OUT/smoke.log

@@ -186,7 +186,7 @@ class Renderer:
     def set_schedule(self, chunk=0, tail_spp=-1, tail_chunk=0):
         check(self.L.rt_ctx_set_schedule(self._h, chunk, tail_spp, tail_chunk), "rt_ctx_set_schedule")
 
-    KERNELS = {"grid": 0, "persistent": 1, "auto": 2}  # RT_KERNEL_* (include/rtmi.h)
+    KERNELS = {"grid": 0, "persistent": 1, "auto": 2, "queue": 3}  # RT_KERNEL_* (include/rtmi.h)
 
     def set_kernel(self, kind="auto"):
         check(self.L.rt_ctx_set_kernel(self._h, self.KERNELS[kind]), "rt_ctx_set_kernel")

@@ -268,11 +268,14 @@ __device__ __forceinline__ void flush_counters(const SegCounters &cnt, int lane,
 // absorption, or the scattered ray with its robustness offset.  Returns true
 // when the path ended: col is then its colour (black when absorbed or out of
 // depth).  Shared by every fast kernel, so they compute identical paths.
-template <int ACC>
+// FROM_BIG (the queue kernel): the grid's big-sphere pass was run when the
+// ray was made; its result (t_max0, best0) starts the walk.
+template <int ACC, bool FROM_BIG = false>
 __device__ __forceinline__ bool path_segment(const SceneView<float> &sc, const SpherePair *__restrict__ pairs,
                                              const RenderArgs &a, V3<float> &o, V3<float> &d, V3<float> &T,
                                              int &depth, Xoro &rng, V3<float> &col, SegCounters &cnt,
-                                             unsigned long long *segments) {
+                                             unsigned long long *segments, float t_max0 = INFINITY,
+                                             int32_t best0 = -1) {
   (void)cnt, (void)segments;
   float t;
 #if RTMI_TRACE
@@ -287,14 +290,14 @@ __device__ __forceinline__ bool path_segment(const SceneView<float> &sc, const S
 #endif
     );
   } else if constexpr (ACC >= 2) {
-    k = hit_world_grid<kBigGroup, ACC == 3>(a.acc, o, d, t, key
+    k = hit_world_grid<kBigGroup, ACC == 3, FROM_BIG>(a.acc, o, d, t, key
 #if RTMI_STATS
                                    , cnt.bvh_stats
 #endif
 #if RTMI_TRACE_PHASES
                                    , cnt.pc
 #endif
-    );
+                                   , t_max0, best0);
   } else {
     k = hit_world_packed<kPairGroup>(pairs, a.npairs, o, d, t
 #if RTMI_STATS
@@ -855,6 +858,465 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
   (void)n_taken;
 }
 
+// ---------------------------------------------------------------------------
+// queue kernel: CU-resident 16-wave blocks sharing one LDS pool of rays,
+// binned by the pre-walk bound
+// ---------------------------------------------------------------------------
+// The grid kernel's waves each walk their own 64 paths: a wave pays for its
+// longest walk, so the walk runs at 0.34 lane utilisation.  Here a block's
+// waves share a pool of kQSlots waiting rays in LDS, kept in kQBins bins by
+// the bound on their next walk's cell count (grid_bound, from the big-sphere
+// pass run when the ray is made).  Each pass a wave picks the fullest bin:
+// lanes whose ray is in it keep it, the others swap theirs for one of that
+// bin's rays, so the wave walks rays of similar length together
+// (tools/grid_sim.c: cell-step lane utilisation 0.35 -> 0.82 with 8 bins of a
+// 512-ray pool).  No wave waits for another: bins are multi-producer /
+// multi-consumer rings of slot indices in LDS (a claim by compare-and-swap on
+// the ring head, a push by atomic add on its tail, entries polled until
+// written), so the only coupling is the pool.  Camera jobs come from block
+// work items (tile, sample range) held in kQItems LDS slots with their
+// fixed-point sums: a ray carries its item slot and pixel, whichever wave ends
+// the path adds its colour there, and the wave that ends an item's last path
+// writes the item out.  Integer sums: the image is bit-identical to every
+// other kernel's, in any order of rays and waves.
+#ifndef RTMI_QUEUE_BINS
+#define RTMI_QUEUE_BINS 8
+#endif
+#ifndef RTMI_QUEUE_SLOTS
+#define RTMI_QUEUE_SLOTS 512
+#endif
+constexpr int kQWaves = 16;
+constexpr int kQBins = RTMI_QUEUE_BINS;
+constexpr int kQSlots = RTMI_QUEUE_SLOTS;
+constexpr int kQFree = kQBins;  // the ring of free slots
+constexpr int kQRings = kQBins + 1;
+constexpr int kQItems = 4;  // item slots per block (2 bits of a ray's meta word)
+constexpr uint32_t kQEmpty = 0xFFFFu;
+constexpr uint32_t kQSpinMax = 1u << 20;  // watchdog: polls of one ring entry
+constexpr uint32_t kQIdleMax = 1u << 20;  // watchdog: passes without a live lane
+// the jobs word: item slot (bits 29-31) | camera jobs handed out (bits 0-28)
+constexpr uint32_t kQJobBits = 29, kQJobMask = (1u << kQJobBits) - 1u;
+constexpr uint32_t kQNone = 4u, kQSwitching = 5u, kQDrained = 6u;  // slot field: no item yet / being replaced / no items left
+static_assert((kQSlots & (kQSlots - 1)) == 0 && kQSlots <= 32768, "ring positions wrap by mask; slot indices are 16-bit");
+static_assert(kQBins >= 2 && kQBins <= 32, "bins");
+
+struct QueueLds {
+  float4 ray[4][kQSlots];         // o|T.x, d|T.y, T.z|t_max|meta|best, xoroshiro state
+  uint16_t ring[kQRings][kQSlots];  // slot indices (kQEmpty: not yet written / consumed)
+  uint32_t head[kQRings], tail[kQRings];
+  unsigned long long acc[kQItems][3][64];  // fixed-point sums per item slot
+  int32_t item[kQItems][8];        // x0, y0, vw, nv, s_base + s0, tile, nq, live
+  uint32_t done[kQItems], segs[kQItems];  // paths ended; their segments (the tile's cost)
+  uint32_t jobs;
+};
+
+__device__ __forceinline__ uint32_t q_load(const uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void q_store(uint32_t *p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t q_add(uint32_t *p, uint32_t v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool q_cas(uint32_t *p, uint32_t expected, uint32_t desired) {
+  return __hip_atomic_compare_exchange_strong(p, &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t q_uniform(uint32_t v) { return uint32_t(__builtin_amdgcn_readfirstlane(int(v))); }
+__device__ __forceinline__ int q_rank(unsigned long long m) {
+  return __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
+}
+
+template <int TW, bool FLAT>
+__global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
+    const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1, RenderArgs a,
+    unsigned long long *__restrict__ accum, float *__restrict__ out, unsigned long long *__restrict__ segments,
+    unsigned *__restrict__ counter) {
+  constexpr int ACC = FLAT ? 3 : 2;
+  __shared__ QueueLds Q;
+  __shared__ float cam_lds[21];
+  const int lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < kQRings * kQSlots; i += blockDim.x) {
+    const int r = i / kQSlots, k = i - r * kQSlots;
+    Q.ring[r][k] = uint16_t(r == kQFree ? k : int(kQEmpty));
+  }
+  for (int i = threadIdx.x; i < kQItems * 3 * 64; i += blockDim.x) (&Q.acc[0][0][0])[i] = 0;
+  if (threadIdx.x < kQRings) {
+    Q.head[threadIdx.x] = 0;
+    Q.tail[threadIdx.x] = threadIdx.x == kQFree ? kQSlots : 0;
+  }
+  if (threadIdx.x < kQItems) {
+    Q.item[threadIdx.x][7] = 0;
+    Q.done[threadIdx.x] = 0;
+    Q.segs[threadIdx.x] = 0;
+  }
+  if (threadIdx.x == 0) Q.jobs = kQNone << kQJobBits;
+  stage_camera(cam_lds, a);
+  stage_grid(a.acc);  // (ends with the block barrier: the only one)
+
+  const SceneView<float> sc{geom, sh0, sh1, a.n};
+  SegCounters cnt{};
+  unsigned nseg = 0;
+  bool fault = false;  // a watchdog fired (segments[7]): leave
+
+  // the lane's ray: o, d, T, generator, meta = depth (bits 0-23) | pixel in
+  // the tile (24-29) | item slot (30-31); its big-sphere result (t_max, best:
+  // record-slot key) and bin key
+  V3<float> o = mk(0.f, 0.f, 0.f), d = o, T = o;
+  Xoro rng{0, 0};
+  int meta = 0, best = -1, key = 0;
+  float tmax = 0.f;
+  bool has = false, prep = false;
+
+  // ---- ring operations --------------------------------------------------
+  // Claim up to `want` entries of ring r (wave-level; head and tail are read
+  // again after a failed compare-and-swap).  Returns the count, h the first.
+  auto claim = [&](int r, int want, uint32_t &h) {
+    uint32_t hh = 0, nn = 0;
+    if (lane == 0) {
+      for (int tries = 0; tries < 256; ++tries) {
+        hh = q_load(&Q.head[r]);
+        const int avail = int(q_load(&Q.tail[r]) - hh);
+        nn = uint32_t(max(0, min(want, avail)));
+        if (nn == 0 || q_cas(&Q.head[r], hh, hh + nn)) break;
+        nn = 0;
+      }
+    }
+    h = q_uniform(hh);
+    return int(q_uniform(nn));
+  };
+  // The entry at position pos of ring r, for the lanes with `want`: polled
+  // until its pusher has written it, then marked consumed.
+  auto take = [&](int r, uint32_t pos, bool want) {
+    volatile uint16_t *e = &Q.ring[r][pos & (kQSlots - 1)];
+    uint32_t v = 0;
+    bool pend = want;
+    for (uint32_t spin = 0; __ballot(pend); ++spin) {
+      if (pend) {
+        v = *e;
+        if (v != kQEmpty) {
+          *e = uint16_t(kQEmpty);
+          pend = false;
+        }
+      }
+      if (spin > kQSpinMax) {
+        fault = true;
+        pend = false;
+      }
+      if (__ballot(pend)) __builtin_amdgcn_s_sleep(1);
+    }
+    return v;
+  };
+  // Push slot s onto ring r (lanes with `want`): a tail position, polled until
+  // its previous entry has been consumed, then written.
+  auto put = [&](int r, uint32_t s, bool want) {
+    uint32_t pos = 0;
+    if (want) pos = q_add(&Q.tail[r], 1u);
+    volatile uint16_t *e = &Q.ring[r][pos & (kQSlots - 1)];
+    bool pend = want;
+    for (uint32_t spin = 0; __ballot(pend); ++spin) {
+      if (pend && *e == kQEmpty) {
+        *e = uint16_t(s);
+        pend = false;
+      }
+      if (spin > kQSpinMax) {
+        fault = true;
+        pend = false;
+      }
+      if (__ballot(pend)) __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  auto store_ray = [&](uint32_t s) {
+    Q.ray[0][s] = make_float4(o.x, o.y, o.z, T.x);
+    Q.ray[1][s] = make_float4(d.x, d.y, d.z, T.y);
+    Q.ray[2][s] = make_float4(T.z, tmax, __int_as_float(meta), __int_as_float(best));
+    Q.ray[3][s] = make_float4(__uint_as_float(uint32_t(rng.s0)), __uint_as_float(uint32_t(rng.s0 >> 32)),
+                              __uint_as_float(uint32_t(rng.s1)), __uint_as_float(uint32_t(rng.s1 >> 32)));
+  };
+
+  // ---- camera jobs ------------------------------------------------------
+  // The wave's camera-ray pool (as render_kernel's): lane L holds the camera
+  // ray of one claimed job, slots [ppos, pn) not yet taken.
+  V3<float> po = o, pd = o;
+  Xoro prng{0, 0};
+  int pn = 0, ppos = 0;    // wave-uniform
+  // the pool's jobs (wave-uniform): item slot, first job, pixels of the tile
+  // (a taken ray's meta word is recomputed from these, not carried per lane)
+  int p_slot = 0, p_j0 = 0, p_nv = 1;
+  bool drained = false;   // no block work item left
+  // Claim the next 64 camera jobs of the block's current item (moving the
+  // block to its next item when this one is handed out) and make their rays.
+  auto refill = [&]() {
+    for (int attempt = 0; attempt < 8; ++attempt) {
+      const uint32_t v = q_uniform(q_load(&Q.jobs));
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the item fields after the word naming them
+      const uint32_t s = v >> kQJobBits;
+      if (s == kQDrained) {
+        drained = true;
+        return false;
+      }
+      if (s == kQSwitching) return false;  // another wave is fetching the next item
+      if (s < kQItems && int(v & kQJobMask) < Q.item[s][6]) {
+        uint32_t old = 0;
+        if (lane == 0) old = q_add(&Q.jobs, 64u);
+        old = q_uniform(old);
+        const uint32_t s2 = old >> kQJobBits;
+        if (s2 >= kQItems) continue;  // the word changed state meanwhile (this add is overwritten)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const int j0 = int(old & kQJobMask);
+        const int x0 = Q.item[s2][0], y0 = Q.item[s2][1], vw = Q.item[s2][2], nv = Q.item[s2][3];
+        const int sbase = Q.item[s2][4], nq = Q.item[s2][6];
+        if (j0 >= nq) continue;
+        pn = min(64, nq - j0);
+        ppos = 0;
+        p_slot = int(s2);
+        p_j0 = j0;
+        p_nv = nv;
+        if (lane < pn) {
+          // job q -> pixel q % nv, sample q / nv (q < nq <= 64 * 65535 < 2^22: div_small is exact)
+          const int q = j0 + lane;
+          const int qs = div_small(q, nv, 1.0f / float(nv));
+          const int p = q - qs * nv;
+          const int ly = div_small(p, vw, 1.0f / float(vw)), lx = p - ly * vw;
+          const int i = x0 + lx;
+          const int j = a.row0 + (y0 + ly) * a.row_step;
+          prng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(sbase + qs));
+          float ju, jv;
+          prng.pair(ju, jv);
+          const float u = (float(i) + ju) * cam_lds[19];  // main.cpp:278, by the reciprocal
+          const float vv = (float(j) + jv) * cam_lds[20];  // main.cpp:279
+          get_ray<true, float>(lds_camera(cam_lds), u, vv, prng, po, pd);
+        }
+        return true;
+      }
+      // handed out (or no item yet): fetch the next item into a free slot
+      uint32_t won = 0;
+      if (lane == 0) won = q_cas(&Q.jobs, v, kQSwitching << kQJobBits) ? 1u : 0u;
+      if (!q_uniform(won)) continue;
+      int f = -1;
+      for (int k = 0; k < kQItems && f < 0; ++k)
+        if (q_uniform(q_load(reinterpret_cast<uint32_t *>(&Q.item[k][7]))) == 0) f = k;
+      if (f < 0) {  // every slot still has paths in flight: retry later
+        if (lane == 0) q_store(&Q.jobs, v);
+        return false;
+      }
+      for (;;) {
+        unsigned itn = 0;
+        if (lane == 0) itn = atomicAdd(counter, 1u);
+        itn = q_uniform(itn);
+        if (int(itn) >= a.n_items) {
+          if (lane == 0) q_store(&Q.jobs, kQDrained << kQJobBits);
+          drained = true;
+          return false;
+        }
+        const ItemDesc cd = describe_item<TW>(a, int(itn));
+        if (cd.nq <= 0) continue;  // an empty item: nothing to render
+        if (lane < 8) {
+          const int fld[8] = {cd.x0, cd.y0, cd.vw, cd.nv, a.s_base + cd.s0, cd.tile, cd.nq, 1};
+          int x = fld[0];
+#pragma unroll
+          for (int k = 1; k < 8; ++k) x = lane == k ? fld[k] : x;
+          Q.item[f][lane] = x;
+        }
+        if (lane == 0) {
+          Q.done[f] = 0;
+          Q.segs[f] = 0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) q_store(&Q.jobs, uint32_t(f) << kQJobBits);
+        break;
+      }
+    }
+    return false;
+  };
+
+  // An item slot whose paths have all ended: its sums to the output (the
+  // floats when the item covers every sample of its tile, else the global
+  // fixed-point accumulator), its cost to the tile's, then the slot is free.
+  auto flush = [&](int s) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const int x0 = Q.item[s][0], y0 = Q.item[s][1], vw = Q.item[s][2], nv = Q.item[s][3], tile = Q.item[s][5];
+    unsigned long long v[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      v[c] = Q.acc[s][c][lane];
+      Q.acc[s][c][lane] = 0;
+    }
+    if (lane < nv) {
+      const int ly = lane / vw, lx = lane - ly * vw;
+      const size_t o3 = (size_t(y0 + ly) * size_t(a.W) + size_t(x0 + lx)) * 3;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        if (a.block_owns_tile) out[o3 + c] = from_fixed((long long)v[c]);
+        else atomicAdd(&accum[o3 + c], v[c]);
+      }
+    }
+    if (lane == 0 && a.tile_cost) atomicAdd(&a.tile_cost[tile], q_load(&Q.segs[s]));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) q_store(reinterpret_cast<uint32_t *>(&Q.item[s][7]), 0u);
+  };
+
+  auto pull = [](int src4, float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(src4, __float_as_int(v))); };
+  auto pull64 = [](int src4, uint64_t v) {
+    const uint32_t lo = uint32_t(__builtin_amdgcn_ds_bpermute(src4, int(uint32_t(v))));
+    const uint32_t hi = uint32_t(__builtin_amdgcn_ds_bpermute(src4, int(uint32_t(v >> 32))));
+    return (uint64_t(hi) << 32) | lo;
+  };
+
+  uint32_t idle = 0;
+  for (;;) {
+    // 1. empty lanes take camera rays
+    unsigned long long empty = __ballot(!has);
+    while (empty) {
+      if (ppos >= pn && (drained || !refill())) break;
+      const int rank = q_rank(empty);
+      const int take_n = min(__popcll(empty), pn - ppos);
+      const int src4 = ((ppos + rank) & 63) << 2;
+      const V3<float> ro = mk(pull(src4, po.x), pull(src4, po.y), pull(src4, po.z));
+      const V3<float> rd = mk(pull(src4, pd.x), pull(src4, pd.y), pull(src4, pd.z));
+      Xoro g;
+      g.s0 = pull64(src4, prng.s0);
+      g.s1 = pull64(src4, prng.s1);
+      if (!has && rank < take_n) {
+        const int q = p_j0 + ((ppos + rank) & 63);
+        const int p = q - div_small(q, p_nv, 1.0f / float(p_nv)) * p_nv;
+        o = ro;
+        d = rd;
+        rng = g;
+        meta = (p_slot << 30) | (p << 24);
+        T = mk(1.f, 1.f, 1.f);
+        has = true;
+        prep = true;
+      }
+      ppos = __builtin_amdgcn_readfirstlane(ppos + take_n);
+      empty = __ballot(!has);
+    }
+    // 2. new rays (camera or scattered): the big spheres, then the bin key
+    if (prep) {
+      grid_big<kBigGroup>(a.acc, o, d, tmax, best
+#if RTMI_STATS
+                          , cnt.bvh_stats
+#endif
+      );
+      key = min(grid_bound<FLAT>(o, d, tmax), kQBins - 1);
+      prep = false;
+    }
+    // 3. the exchange: the fullest bin's rays for the lanes not holding one
+    {
+      uint32_t c = 0;
+      if (lane < kQBins) c = q_load(&Q.tail[lane]) - q_load(&Q.head[lane]);
+      int bs = 0;
+      uint32_t bc = uint32_t(__builtin_amdgcn_readlane(int(c), 0));
+#pragma unroll
+      for (int b = 1; b < kQBins; ++b) {
+        const uint32_t cb = uint32_t(__builtin_amdgcn_readlane(int(c), b));
+        if (cb > bc) {
+          bc = cb;
+          bs = b;
+        }
+      }
+      const bool keep = has && key == bs;
+      const unsigned long long tm = __ballot(!has), lm = __ballot(has && !keep);
+      const int nt = __popcll(tm);
+      uint32_t h = 0;
+      const int n = (tm | lm) && bc ? claim(bs, nt + __popcll(lm), h) : 0;
+      // empty lanes first (an idle lane costs more than one holding another bin's ray)
+      const int rank = has ? nt + q_rank(lm) : q_rank(tm);
+      const bool got = !keep && rank < n;
+      const uint32_t slot = take(bs, h + uint32_t(rank), got) & (kQSlots - 1);
+      // leavers without a partner park their ray in a free slot (filling the pool)
+      const bool park_want = has && !keep && !got;
+      const unsigned long long pm = __ballot(park_want);
+      uint32_t hf = 0;
+      const int nf = pm ? claim(kQFree, __popcll(pm), hf) : 0;
+      const int prank = q_rank(pm);
+      const bool park = park_want && prank < nf;
+      const uint32_t fslot = take(kQFree, hf + uint32_t(prank), park) & (kQSlots - 1);
+      int push_ring = -1;
+      uint32_t push_slot = 0;
+      if (got) {
+        // quarter by quarter (one quarter of a second ray live at a time):
+        // read the slot's quarter, write the lane's own there, take the read one
+        push_ring = has ? key : kQFree;
+        push_slot = slot;
+        const float4 r0 = Q.ray[0][slot];
+        if (has) Q.ray[0][slot] = make_float4(o.x, o.y, o.z, T.x);
+        o = mk(r0.x, r0.y, r0.z);
+        T.x = r0.w;
+        const float4 r1 = Q.ray[1][slot];
+        if (has) Q.ray[1][slot] = make_float4(d.x, d.y, d.z, T.y);
+        d = mk(r1.x, r1.y, r1.z);
+        T.y = r1.w;
+        const float4 r2 = Q.ray[2][slot];
+        if (has) Q.ray[2][slot] = make_float4(T.z, tmax, __int_as_float(meta), __int_as_float(best));
+        T.z = r2.x;
+        tmax = r2.y;
+        meta = __float_as_int(r2.z);
+        best = __float_as_int(r2.w);
+        const float4 r3 = Q.ray[3][slot];
+        if (has)
+          Q.ray[3][slot] = make_float4(__uint_as_float(uint32_t(rng.s0)), __uint_as_float(uint32_t(rng.s0 >> 32)),
+                                       __uint_as_float(uint32_t(rng.s1)), __uint_as_float(uint32_t(rng.s1 >> 32)));
+        rng.s0 = (uint64_t(__float_as_uint(r3.y)) << 32) | __float_as_uint(r3.x);
+        rng.s1 = (uint64_t(__float_as_uint(r3.w)) << 32) | __float_as_uint(r3.z);
+        has = true;
+      }
+      if (park) {
+        store_ray(fslot);
+        push_ring = key;
+        push_slot = fslot;
+        has = false;
+      }
+      // the ray writes (and the reads of swapped-out slots) before the pushes
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      for (int r = 0; r < kQRings; ++r)
+        if (__ballot(push_ring == r)) put(r, push_slot, push_ring == r);
+    }
+    const unsigned long long live = __ballot(has);
+    if (live == 0) ++idle;
+    if (__ballot(fault) || idle > kQIdleMax) {
+      if (lane == 0) atomicOr(&segments[7], 1ull << 63);  // watchdog: the host reports RT_EHIP
+      break;
+    }
+    if (live == 0) {
+      if (drained && ppos >= pn) {
+        uint32_t c = 0;
+        if (lane < kQBins) c = q_load(&Q.tail[lane]) - q_load(&Q.head[lane]);
+        if (__ballot(c != 0) == 0) break;  // no rays left anywhere this wave could take
+      }
+      __builtin_amdgcn_s_sleep(4);
+      continue;
+    }
+    idle = 0;
+    nseg = unsigned(__builtin_amdgcn_readfirstlane(int(nseg + unsigned(__popcll(live)))));
+    // 4. one segment of every held ray, from its big-sphere result
+    bool done = false;
+    V3<float> col = mk(0.f, 0.f, 0.f);
+    if (has) done = path_segment<ACC, true>(sc, nullptr, a, o, d, T, meta, rng, col, cnt, segments, tmax, best);
+    // 5. ended paths: colour to their item's sums; the item's last path flushes it
+    int cs = 0;
+    if (done) {
+      cs = int(uint32_t(meta) >> 30);
+      const int p = (meta >> 24) & 63;
+      atomicAdd(&Q.acc[cs][0][p], (unsigned long long)to_fixed(col.x));
+      atomicAdd(&Q.acc[cs][1][p], (unsigned long long)to_fixed(col.y));
+      atomicAdd(&Q.acc[cs][2][p], (unsigned long long)to_fixed(col.z));
+      q_add(&Q.segs[cs], uint32_t(meta & 0xFFFFFF) + 1u);
+      has = false;
+    } else if (has) {
+      prep = true;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the sums before the count
+    bool complete = false;
+    if (done) complete = int(q_add(&Q.done[cs], 1u)) + 1 == Q.item[cs][6];
+    for (unsigned long long cm = __ballot(complete); cm; cm &= cm - 1)
+      flush(__builtin_amdgcn_readlane(cs, int(__builtin_ctzll(cm))));
+  }
+  if (lane == 0) atomicAdd(segments, (unsigned long long)nseg);
+  flush_counters(cnt, lane, segments);
+}
+
 // Closest hit of n given rays by the brute-force loop and by the BVH
 // (validation: rt_ctx_debug_hits).  rays = {o.xyz, d.xyz} per ray.
 template <int ACC>
@@ -988,6 +1450,9 @@ struct rt_ctx {
   size_t pass_cap = 0;
   int32_t pass_W = 0, pass_rows = 0, pass_spp = 0;
   int32_t resident_blocks = 0;             // blocks of the persistent grid (from the occupancy query)
+  int32_t cu_count = 0;                    // compute units of the device
+  int32_t queue_blocks = 0;                // resident render_queue blocks for queue_lds dynamic LDS bytes
+  size_t queue_lds = 0;
   // BVH, built by rt_ctx_set_scene
   int32_t accel = RT_ACCEL_GRID;  // the fastest structure (brute force when the scene has none)
   SpherePair *big_pairs = nullptr;
@@ -1131,6 +1596,7 @@ RTMI_EXPORT int rt_ctx_create(int32_t device, rt_ctx **out) {
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_persistent<8, true>,
                                                          64 * kWavesPerBlock, 0));
     ctx->resident_blocks = std::max(1, per_cu) * prop.multiProcessorCount;
+    ctx->cu_count = prop.multiProcessorCount;
   }
   *out = ctx.release();
   return RT_OK;
@@ -1522,7 +1988,7 @@ RTMI_EXPORT int rt_ctx_set_schedule(rt_ctx *ctx, int32_t chunk, int32_t tail_spp
 
 RTMI_EXPORT int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind) {
   if (!ctx) return set_error(RT_EINVAL, "null ctx");
-  if (kind != RT_KERNEL_GRID && kind != RT_KERNEL_PERSISTENT && kind != RT_KERNEL_AUTO)
+  if (kind != RT_KERNEL_GRID && kind != RT_KERNEL_PERSISTENT && kind != RT_KERNEL_AUTO && kind != RT_KERNEL_QUEUE)
     return set_error(RT_EINVAL, "unknown kernel kind");
   ctx->kernel = kind;
   return RT_OK;
@@ -1603,6 +2069,31 @@ void launch_tw(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const
                        ctx->sh0, ctx->sh1, ctx->pairs, b, accum, out, ctx->segments);
 }
 
+// resident blocks of the queue kernel with dyn bytes of dynamic LDS (the grid)
+int queue_resident_blocks(rt_ctx *ctx, size_t dyn) {
+  if (ctx->queue_blocks <= 0 || ctx->queue_lds != dyn) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_queue<8, true>, 64 * kQWaves, dyn) !=
+        hipSuccess)
+      per_cu = 0;
+    ctx->queue_blocks = std::max(1, per_cu) * std::max(1, ctx->cu_count);
+    ctx->queue_lds = dyn;
+  }
+  return ctx->queue_blocks;
+}
+
+template <int TW>
+void launch_queue(int acc, dim3 grid, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a,
+                  unsigned long long *accum, float *out) {
+  const size_t lds = accel_lds_bytes(a.acc, acc);
+  if (acc == 3)
+    hipLaunchKernelGGL((render_queue<TW, true>), grid, dim3(64 * kQWaves), lds, st, ctx->geom, ctx->sh0, ctx->sh1, a,
+                       accum, out, ctx->segments, ctx->counter);
+  else
+    hipLaunchKernelGGL((render_queue<TW, false>), grid, dim3(64 * kQWaves), lds, st, ctx->geom, ctx->sh0, ctx->sh1, a,
+                       accum, out, ctx->segments, ctx->counter);
+}
+
 template <int TW>
 void launch_shape(bool persistent, int acc, bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx,
                   const RenderArgs &a, unsigned long long *accum, float *out) {
@@ -1669,6 +2160,9 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
                            ? 1
                            : (ctx->accel == RT_ACCEL_GRID && ctx->grid_ok ? (ctx->grid.n[1] == 1 ? 3 : 2) : 0);
   const bool bvh = acc_kind != 0;
+  // the queue kernel: grid scenes, when selected
+  const bool queue = acc_kind >= 2 && ctx->kernel == RT_KERNEL_QUEUE && TW <= 16;
+  const int64_t qblocks = queue ? queue_resident_blocks(ctx, accel_lds_bytes(accel_of(ctx, acc_kind), acc_kind)) : 0;
   // the persistent kernel runs brute-force scenes only (see the note above stage_camera)
   const bool persistent = !bvh && (ctx->kernel == RT_KERNEL_PERSISTENT ||
                                    (ctx->kernel == RT_KERNEL_AUTO && tile_samples < 6000000));
@@ -1677,6 +2171,11 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     // ~28 items per resident wave (1/8 strip: chunk 8 -> 17.5 ms, 16 -> 17.9, 32 -> 19.7)
     const int64_t waves = int64_t(ctx->resident_blocks) * kWavesPerBlock;
     chunk1 = int32_t(std::min<int64_t>(64, std::max<int64_t>(4, tile_samples / (28 * waves))));
+  } else if (chunk1 <= 0 && queue) {
+    // at least 16 items per resident block (whole tiles when there are that
+    // many tiles: the block writes the floats, no accumulator)
+    const int64_t nch = std::max<int64_t>(1, (16 * qblocks + tiles - 1) / tiles);
+    chunk1 = int32_t(std::max<int64_t>(1, (spp + nch - 1) / nch));
   } else if (chunk1 <= 0) {
     // ~60 k items of 24..125 samples (BVH, cost order, block flush; the
     // rounding below keeps a multiple of 4 items per tile): config 2 runs
@@ -1688,7 +2187,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     chunk1 = int32_t(std::min<int64_t>(125, std::max<int64_t>(ctx->item_min, tile_samples / want_items)));
   }
   if (chunk2 <= 0) chunk2 = std::max(1, chunk1 / 4);
-  if (tail < 0) tail = 0;  // automatic: no short-item phase (it measured no better)
+  if (tail < 0 || queue) tail = 0;  // automatic: no short-item phase (it measured no better)
   // at most 65535 samples per item: job indices (< 64 * chunk) stay below
   // 2^22, where the kernels' float-reciprocal division (div_small) is exact
   chunk1 = std::min({chunk1, spp, 65535});
@@ -1697,7 +2196,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   const int32_t spp1 = spp - tail;
   const int64_t grid_wpb = bvh ? GridShape<true>::waves : GridShape<false>::waves;
   int32_t nch1 = spp1 > 0 ? (spp1 + chunk1 - 1) / chunk1 : 0;
-  if (ctx->chunk <= 0 && !persistent && spp1 >= grid_wpb) {
+  if (ctx->chunk <= 0 && !persistent && !queue && spp1 >= grid_wpb) {
     // automatic grid schedule: exactly a multiple of the block's waves items
     // per tile, so a block's items share a tile and it flushes once
     // (block_flush).  chunk1 = ceil(spp1 / n1) can leave the last items of a
@@ -1729,12 +2228,14 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   a.tiles = int32_t(tiles); a.spp1 = spp1; a.chunk1 = chunk1; a.nch1 = nch1; a.chunk2 = chunk2; a.nch2 = nch2;
   // block flush: every block's items are of one tile — both phases hold a
   // multiple of the block's waves items per tile
-  a.block_flush = !persistent && nch1 % grid_wpb == 0 && nch2 % grid_wpb == 0 && ctx->block_flush;
+  a.block_flush = !persistent && !queue && nch1 % grid_wpb == 0 && nch2 % grid_wpb == 0 && ctx->block_flush;
   a.block_owns_tile = a.block_flush && !pass_accum && nch1 == grid_wpb && nch2 == 0 && ctx->block_owns;
+  // the queue kernel: an item that covers all its tile's samples writes the floats
+  if (queue) a.block_owns_tile = !pass_accum && nch1 == 1 && nch2 == 0 && ctx->block_owns;
   const bool chunked = pass_accum || nch1 + nch2 > 1;
   if (!ctx->probing) {
-    const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush + a.block_owns_tile, persistent ? 0 : 1, persistent ? 1 : 0,
-                              acc_kind == 3 ? 2 : acc_kind};
+    const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush + a.block_owns_tile, persistent ? 0 : 1,
+                              queue ? 2 : (persistent ? 1 : 0), acc_kind == 3 ? 2 : acc_kind};
     std::copy(sched, sched + 8, ctx->last_sched);
   }
   a.s_base = s_base;
@@ -1819,7 +2320,15 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   if (chunked && !pass_accum && !a.block_owns_tile)
     HIP_TRY(hipMemsetAsync(ctx->accum, 0, n_valid_out * sizeof(unsigned long long), st));
   dim3 grid;
-  if (persistent) {
+  if (queue) {
+    // CU-resident blocks pulling work items from a global counter
+    HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
+    grid = dim3(unsigned(std::min<int64_t>(items, qblocks)));
+    switch (TW) {
+      case 8: launch_queue<8>(acc_kind, grid, st, ctx, a, accum, strip); break;
+      default: launch_queue<16>(acc_kind, grid, st, ctx, a, accum, strip); break;
+    }
+  } else if (persistent) {
     // a resident grid of waves pulling items from a global counter
     HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
     const int64_t pw = kWavesPerBlock;
@@ -1829,7 +2338,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     const int64_t wpb = bvh ? GridShape<true>::waves : GridShape<false>::waves;
     grid = dim3(unsigned((items + wpb - 1) / wpb));
   }
-  switch (TW) {
+  if (!queue) switch (TW) {
     case 8: launch_shape<8>(persistent, acc_kind, chunked, grid, st, ctx, a, accum, strip); break;
     case 16: launch_shape<16>(persistent, acc_kind, chunked, grid, st, ctx, a, accum, strip); break;
     case 32: launch_shape<32>(persistent, acc_kind, chunked, grid, st, ctx, a, accum, strip); break;

@@ -492,7 +492,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--tail-spp", type=int, default=-1)
     ap.add_argument("--tail-chunk", type=int, default=0)
-    ap.add_argument("--kernel", choices=["auto", "persistent", "grid"], default="auto")
+    ap.add_argument("--kernel", choices=["auto", "persistent", "grid", "queue"], default="auto")
     ap.add_argument("--accel", choices=["none", "bvh", "grid"], default="grid",
                     help="closest-hit search: grid (default: uniform grid + DDA), bvh or brute force; same image bit for bit")
     ap.add_argument("--ordering", choices=["cost", "none"], default="cost")

@@ -138,8 +138,11 @@ int rt_ctx_set_schedule(rt_ctx *ctx, int32_t chunk, int32_t tail_spp, int32_t ta
  * BVH the grid kernel runs, which measured faster.
  * RT_KERNEL_GRID: one wave per work item.  RT_KERNEL_AUTO (default):
  * persistent for brute-force strips (fewer than 6e6 tile-samples), grid
- * otherwise.  All give bit-identical images. */
-enum { RT_KERNEL_GRID = 0, RT_KERNEL_PERSISTENT = 1, RT_KERNEL_AUTO = 2 };
+ * otherwise.  RT_KERNEL_QUEUE: CU-resident 16-wave blocks that share an LDS
+ * pool of rays binned by the length of their next grid walk (grid scenes,
+ * tiles of 8 or 16 columns; otherwise as RT_KERNEL_AUTO).
+ * All give bit-identical images. */
+enum { RT_KERNEL_GRID = 0, RT_KERNEL_PERSISTENT = 1, RT_KERNEL_AUTO = 2, RT_KERNEL_QUEUE = 3 };
 int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind);
 
 /* Closest-hit search.  RT_ACCEL_NONE: brute force over all spheres, the

@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round 4, second record call: the N>1 rehearsal through bench.py's own
+# The second record call: the N>1 rehearsal through bench.py's own
 # launcher (gloo, N ranks on one GPU), HBM traffic of the BVH and brute-force
-# kernels on the current tree (stale round-1 entries), their
+# kernels on the current tree, their
 # bench lines, and the walk counters + phase clocks (gpu_phases.sh).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-B=${B:-r04_extras}
+B=${B:-extras}
 mkdir -p gpurun_out/$B
 TAG=$B/gloo RANKS="2 3 8" bash tools/gpu_gloo_rehearsal.sh || exit 1
 for acc in bvh none; do

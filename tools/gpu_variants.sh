@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round 4: bit-exactness of library variants (tests/test_gpu_parity.py with
+# Bit-exactness of library variants (tests/test_gpu_parity.py with
 # RTMI_LIBRARY = lib/librtmi_<v>.so, for every v of LIBS except base), then
 # their interleaved A/B on config 2 and the 1/8 strip (tools/gpu_ab_lib.sh).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-OUT=gpurun_out/${TAG:-r04_ab}
+OUT=gpurun_out/${TAG:-variants}
 mkdir -p $OUT
 for v in $LIBS; do
   [ "$v" = base ] && continue
@@ -13,5 +13,5 @@ for v in $LIBS; do
     -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/parity_$v.log 2>&1 || { echo "variant $v: parity FAILED"; tail -20 $OUT/parity_$v.log; exit 1; }
   echo "variant $v: $(tail -1 $OUT/parity_$v.log)"
 done
-TAG=${TAG:-r04_ab}/ab LIBS="$LIBS" bash tools/gpu_ab_lib.sh || exit 1
+TAG=${TAG:-variants}/ab LIBS="$LIBS" bash tools/gpu_ab_lib.sh || exit 1
 python tools/ab_summary.py $OUT/ab "$LIBS"

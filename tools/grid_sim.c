@@ -42,9 +42,9 @@ static double rnd(void) {
   return (rs >> 11) * (1.0 / 9007199254740992.0);
 }
 
-typedef struct { double o[3], d[3]; int depth; } Ray;
+typedef struct { double o[3], d[3]; int depth, path; } Ray;
 static unsigned long long *g_cand, *g_use;
-static Ray *segs; static int nseg, capseg, cur_depth;
+static Ray *segs; static int nseg, capseg, cur_depth, cur_path;
 static int *tile_start; static int ntiles, captiles;
 
 static int hit_bf(const double o[3], const double d[3], double *tt) {
@@ -70,7 +70,7 @@ static void rand_unit(double v[3]) {
 
 static void push(const double o[3], const double d[3]) {
   if (nseg == capseg) { capseg = capseg ? 2*capseg : 1<<20; segs = realloc(segs, capseg*sizeof(Ray)); }
-  memcpy(segs[nseg].o, o, 24); memcpy(segs[nseg].d, d, 24); segs[nseg].depth = cur_depth; nseg++;
+  memcpy(segs[nseg].o, o, 24); memcpy(segs[nseg].d, d, 24); segs[nseg].depth = cur_depth; segs[nseg].path = cur_path; nseg++;
 }
 
 /* ---- grid (build_grid's shape: small spheres, margin-grown boxes, ~0.3 cells per sphere) ---- */
@@ -336,6 +336,79 @@ static void regroup_cost(int block, double E) {
   free(ids); free(walkers);
 }
 
+/* The barrier-free LDS ray queue, modelled.  A
+ * CU-resident block keeps a pool of P waiting rays in LDS, binned by the
+ * pre-walk bound (min(bound, NB-1); bound 0 = no walk).  A wave pops 64 rays
+ * from the fullest bin (topped up from the next fullest when it has fewer),
+ * runs one segment of each (big spheres are done at push time, so the walk
+ * and shading follow at once), and pushes the survivors back by the bound of
+ * their next segment; an ended path is replaced by the next camera ray of
+ * the block's work, pushed by its first segment's bound.  No wave waits for
+ * another: the pool is the only coupling.  Paths are replayed in generation
+ * order (tile by tile, sample-major), each path's segments in depth order.
+ * Cost per wave-pass: CI_REST + the walk of the popped rays + E (push: key,
+ * per-bin ranking, 16 dwords of ray state written; pop: the bin claim and 16
+ * dwords read).  Baseline: today's 64 consecutive segments of the shuffled
+ * stream per wave-pass. */
+static int *pfirst, *plen, npaths;  /* per path: its segments' indices in depth order */
+static int cmp_pd(const void *x, const void *y) {
+  const Ray *a = &segs[*(const int *)x], *b = &segs[*(const int *)y];
+  if (a->path != b->path) return a->path < b->path ? -1 : 1;
+  return a->depth < b->depth ? -1 : a->depth > b->depth;
+}
+static int *pd_order;
+static void build_paths(void) {
+  pd_order = malloc(nseg * sizeof(int));
+  for (int i = 0; i < nseg; i++) pd_order[i] = i;
+  qsort(pd_order, nseg, sizeof(int), cmp_pd);
+  int maxp = 0; for (int i = 0; i < nseg; i++) if (segs[i].path > maxp) maxp = segs[i].path;
+  npaths = maxp + 1;
+  pfirst = calloc(npaths, sizeof(int)); plen = calloc(npaths, sizeof(int));
+  for (int i = 0; i < nseg; i++) { int p = segs[pd_order[i]].path; if (plen[p]++ == 0) pfirst[p] = i; }
+}
+static int qbox;  /* 1: key on the grid-box bound alone (no big-sphere pass before the key) */
+static int qkey(int seg, int NB) { int b = qbox ? W[seg].pnb : W[seg].pred; return b >= NB ? NB - 1 : b; }
+static void queue_model(int P, int NB, const double *Es, int nE) {
+  /* bins hold (path, segment cursor) pairs */
+  int cap = P + 64, **bin = malloc(NB * sizeof(int *)), **cur = malloc(NB * sizeof(int *)), *cnt = calloc(NB, sizeof(int));
+  for (int b = 0; b < NB; b++) { bin[b] = malloc(cap * sizeof(int)); cur[b] = malloc(cap * sizeof(int)); }
+  int next_path = 0, pool = 0;
+  Acc acc = {0}; double walk = 0, passes = 0, part = 0;
+  #define QPUSH(p, c) do { int s_ = pd_order[pfirst[p] + (c)], k_ = qkey(s_, NB); bin[k_][cnt[k_]] = (p); cur[k_][cnt[k_]++] = (c); pool++; } while (0)
+  while (pool < P && next_path < npaths) { QPUSH(next_path, 0); next_path++; }
+  int ids[64], pp[64], pc[64];
+  while (pool > 0) {
+    int n = 0;
+    while (n < 64 && pool > 0) {  /* the fullest bin first */
+      int bb = 0; for (int b = 1; b < NB; b++) if (cnt[b] > cnt[bb]) bb = b;
+      while (n < 64 && cnt[bb] > 0) { cnt[bb]--; pool--; pp[n] = bin[bb][cnt[bb]]; pc[n] = cur[bb][cnt[bb]]; n++; }
+      if (pool < 64 - n && next_path >= npaths) { /* the drain: take what is there */ }
+    }
+    if (n < 64) part++;
+    for (int l = 0; l < n; l++) ids[l] = pd_order[pfirst[pp[l]] + pc[l]];
+    wave_cost(ids, n, &acc);
+    walk += walk_instr(ids, n, NULL); passes++;
+    for (int l = 0; l < n; l++) {
+      if (pc[l] + 1 < plen[pp[l]]) QPUSH(pp[l], pc[l] + 1);
+      else if (next_path < npaths) { QPUSH(next_path, 0); next_path++; }
+    }
+  }
+  /* baseline: the shuffled stream, 64 consecutive segments per wave-pass */
+  double bwalk = 0, bpass = 0;
+  for (int i = 0; i < nseg; i += 64) { int nl = nseg - i < 64 ? nseg - i : 64; for (int l = 0; l < nl; l++) ids[l] = i + l; bwalk += walk_instr(ids, nl, NULL); bpass++; }
+  printf("  queue P %4d bins %d: wave cells %.3f spheres %.3f per wave-seg (util %.3f / %.3f), walk %.1f -> %.1f instr/wave-pass (%.3f), part-filled pops %.4f;",
+         P, NB, acc.wave_cells * 64 / nseg, acc.wave_spheres * 64 / nseg, acc.lane_cells / (64 * acc.wave_cells),
+         acc.lane_spheres / (64 * acc.wave_spheres), bwalk / bpass, walk / passes, (walk / passes) / (bwalk / bpass), part / passes);
+  for (int e = 0; e < nE; e++) {
+    const double base = CI_REST * bpass + bwalk, q = (CI_REST + Es[e]) * passes + walk;
+    printf(" E %3.0f: net %+.1f%%", Es[e], 100 * (q / base - 1));
+  }
+  printf("\n");
+  for (int b = 0; b < NB; b++) { free(bin[b]); free(cur[b]); }
+  free(bin); free(cur); free(cnt);
+  #undef QPUSH
+}
+
 int main(int argc, char **argv) {
   FILE *f = fopen(argc > 1 ? argv[1] : "tests/golden/scene_final.txt", "r");
   if (!f || fscanf(f, "%d", &N) != 1) return 1;
@@ -358,6 +431,7 @@ int main(int argc, char **argv) {
       for (int a = 0; a < 3; a++) { o[a] = org[a] + cu[a]*dx + cv[a]*dy; d[a] = llc[a] + u*hor[a] + v*ver[a] - o[a]; }
       for (int depth = 0; depth < 50; depth++) {
         cur_depth = depth; push(o, d);
+        if (depth == 0) cur_path++;
         double t; int k = hit_bf(o, d, &t);
         if (k < 0) break;
         double pp[3], nn[3], r = C[k][3];
@@ -479,6 +553,17 @@ int main(int argc, char **argv) {
     printf("\n");
   }
   if (getenv("CI_REST")) CI_REST = atof(getenv("CI_REST"));
+  if (getenv("QUEUE_ONLY")) {
+    build_paths();
+    const double Es[4] = {0, 60, 100, 140};
+    printf("  (%d paths)\n", npaths);
+    for (qbox = 0; qbox <= 1; qbox++) {
+      printf("  key: %s\n", qbox ? "grid-box bound (before the big spheres)" : "bound after the big spheres");
+      for (int NB = 4; NB <= 16; NB *= 2)
+        for (int P = 256; P <= 1024; P *= 2) queue_model(P, NB, Es, 4);
+    }
+    return 0;
+  }
   for (int block = 256; block <= 512; block *= 2)
     for (double E = 0; E <= 120; E += 40) regroup_cost(block, E);
   const char *kn[7] = {"oct", "cell", "oct+cell", "len", "bound", "bound15", "boxbound"};

@@ -891,18 +891,23 @@ constexpr int kQSlots = RTMI_QUEUE_SLOTS;
 constexpr int kQFree = kQBins;  // the ring of free slots
 constexpr int kQRings = kQBins + 1;
 constexpr int kQItems = 4;  // item slots per block (2 bits of a ray's meta word)
-constexpr uint32_t kQEmpty = 0xFFFFu;
+constexpr uint32_t kQEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kQSpinMax = 1u << 20;  // watchdog: polls of one ring entry
 constexpr uint32_t kQIdleMax = 1u << 20;  // watchdog: passes without a live lane
 // the jobs word: item slot (bits 29-31) | camera jobs handed out (bits 0-28)
 constexpr uint32_t kQJobBits = 29, kQJobMask = (1u << kQJobBits) - 1u;
 constexpr uint32_t kQNone = 4u, kQSwitching = 5u, kQDrained = 6u;  // slot field: no item yet / being replaced / no items left
 static_assert((kQSlots & (kQSlots - 1)) == 0 && kQSlots <= 32768, "ring positions wrap by mask; slot indices are 16-bit");
+// A ring entry is (lap << 16 | slot index), lap = position / kQSlots mod 2^16:
+// a slow consumer of position t must not take the value a pusher of t +
+// kQSlots wrote there first (its pushers and consumers can be a lap apart
+// once other waves recycle slots), so a consumer waits for its own lap's tag
+// and a pusher writes only into an empty entry, by compare-and-swap.
 static_assert(kQBins >= 2 && kQBins <= 32, "bins");
 
 struct QueueLds {
   float4 ray[4][kQSlots];         // o|T.x, d|T.y, T.z|t_max|meta|best, xoroshiro state
-  uint16_t ring[kQRings][kQSlots];  // slot indices (kQEmpty: not yet written / consumed)
+  uint32_t ring[kQRings][kQSlots];  // lap << 16 | slot index (kQEmpty: not yet written / consumed)
   uint32_t head[kQRings], tail[kQRings];
   unsigned long long acc[kQItems][3][64];  // fixed-point sums per item slot
   int32_t item[kQItems][8];        // x0, y0, vw, nv, s_base + s0, tile, nq, live
@@ -939,7 +944,7 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
   const int lane = threadIdx.x & 63;
   for (int i = threadIdx.x; i < kQRings * kQSlots; i += blockDim.x) {
     const int r = i / kQSlots, k = i - r * kQSlots;
-    Q.ring[r][k] = uint16_t(r == kQFree ? k : int(kQEmpty));
+    Q.ring[r][k] = r == kQFree ? uint32_t(k) : kQEmpty;  // the free ring: lap 0, every slot
   }
   for (int i = threadIdx.x; i < kQItems * 3 * 64; i += blockDim.x) (&Q.acc[0][0][0])[i] = 0;
   if (threadIdx.x < kQRings) {
@@ -967,7 +972,7 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
   Xoro rng{0, 0};
   int meta = 0, best = -1, key = 0;
   float tmax = 0.f;
-  bool has = false, prep = false;
+  bool has = false;
 
   // ---- ring operations --------------------------------------------------
   // Claim up to `want` entries of ring r (wave-level; head and tail are read
@@ -977,7 +982,8 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
     if (lane == 0) {
       for (int tries = 0; tries < 256; ++tries) {
         hh = q_load(&Q.head[r]);
-        const int avail = int(q_load(&Q.tail[r]) - hh);
+        const uint32_t tt = q_load(&Q.tail[r]);
+        const int avail = int(tt - hh);
         nn = uint32_t(max(0, min(want, avail)));
         if (nn == 0 || q_cas(&Q.head[r], hh, hh + nn)) break;
         nn = 0;
@@ -986,17 +992,19 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
     h = q_uniform(hh);
     return int(q_uniform(nn));
   };
-  // The entry at position pos of ring r, for the lanes with `want`: polled
-  // until its pusher has written it, then marked consumed.
+  // The slot index at position pos of ring r, for the lanes with `want`:
+  // polled until the entry carries this position's lap, then marked consumed.
   auto take = [&](int r, uint32_t pos, bool want) {
-    volatile uint16_t *e = &Q.ring[r][pos & (kQSlots - 1)];
+    volatile uint32_t *e = &Q.ring[r][pos & (kQSlots - 1)];
+    const uint32_t lap = (pos / uint32_t(kQSlots)) & 0xFFFFu;
     uint32_t v = 0;
     bool pend = want;
     for (uint32_t spin = 0; __ballot(pend); ++spin) {
       if (pend) {
-        v = *e;
-        if (v != kQEmpty) {
-          *e = uint16_t(kQEmpty);
+        const uint32_t x = *e;
+        if ((x >> 16) == lap) {
+          *e = kQEmpty;
+          v = x & 0xFFFFu;
           pend = false;
         }
       }
@@ -1008,18 +1016,16 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
     }
     return v;
   };
-  // Push slot s onto ring r (lanes with `want`): a tail position, polled until
-  // its previous entry has been consumed, then written.
+  // Push slot s onto ring r (per lane; lanes with `want`): a tail position,
+  // polled until its previous entry has been consumed, then written.
   auto put = [&](int r, uint32_t s, bool want) {
     uint32_t pos = 0;
     if (want) pos = q_add(&Q.tail[r], 1u);
-    volatile uint16_t *e = &Q.ring[r][pos & (kQSlots - 1)];
+    uint32_t *e = &Q.ring[want ? r : 0][pos & (kQSlots - 1)];
+    const uint32_t val = (((pos / uint32_t(kQSlots)) & 0xFFFFu) << 16) | s;
     bool pend = want;
     for (uint32_t spin = 0; __ballot(pend); ++spin) {
-      if (pend && *e == kQEmpty) {
-        *e = uint16_t(s);
-        pend = false;
-      }
+      if (pend && q_cas(e, kQEmpty, val)) pend = false;
       if (spin > kQSpinMax) {
         fault = true;
         pend = false;
@@ -1036,59 +1042,32 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
   };
 
   // ---- camera jobs ------------------------------------------------------
-  // The wave's camera-ray pool (as render_kernel's): lane L holds the camera
-  // ray of one claimed job, slots [ppos, pn) not yet taken.
-  V3<float> po = o, pd = o;
-  Xoro prng{0, 0};
-  int pn = 0, ppos = 0;    // wave-uniform
-  // the pool's jobs (wave-uniform): item slot, first job, pixels of the tile
-  // (a taken ray's meta word is recomputed from these, not carried per lane)
-  int p_slot = 0, p_j0 = 0, p_nv = 1;
-  bool drained = false;   // no block work item left
-  // Claim the next 64 camera jobs of the block's current item (moving the
-  // block to its next item when this one is handed out) and make their rays.
-  auto refill = [&]() {
+  bool drained = false;  // wave-uniform: no block work item left
+  // Claim up to `want` camera jobs of the block's current item (moving the
+  // block to its next item once this one is handed out).  Returns the count
+  // n (0: none now), with the item slot and the first job.  Wave-uniform.
+  auto claim_jobs = [&](int want, int &slot, int &j0) {
     for (int attempt = 0; attempt < 8; ++attempt) {
       const uint32_t v = q_uniform(q_load(&Q.jobs));
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the item fields after the word naming them
       const uint32_t s = v >> kQJobBits;
       if (s == kQDrained) {
         drained = true;
-        return false;
+        return 0;
       }
-      if (s == kQSwitching) return false;  // another wave is fetching the next item
+      if (s == kQSwitching) return 0;  // another wave is fetching the next item
       if (s < kQItems && int(v & kQJobMask) < Q.item[s][6]) {
         uint32_t old = 0;
-        if (lane == 0) old = q_add(&Q.jobs, 64u);
+        if (lane == 0) old = q_add(&Q.jobs, uint32_t(want));
         old = q_uniform(old);
         const uint32_t s2 = old >> kQJobBits;
         if (s2 >= kQItems) continue;  // the word changed state meanwhile (this add is overwritten)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        const int j0 = int(old & kQJobMask);
-        const int x0 = Q.item[s2][0], y0 = Q.item[s2][1], vw = Q.item[s2][2], nv = Q.item[s2][3];
-        const int sbase = Q.item[s2][4], nq = Q.item[s2][6];
-        if (j0 >= nq) continue;
-        pn = min(64, nq - j0);
-        ppos = 0;
-        p_slot = int(s2);
-        p_j0 = j0;
-        p_nv = nv;
-        if (lane < pn) {
-          // job q -> pixel q % nv, sample q / nv (q < nq <= 64 * 65535 < 2^22: div_small is exact)
-          const int q = j0 + lane;
-          const int qs = div_small(q, nv, 1.0f / float(nv));
-          const int p = q - qs * nv;
-          const int ly = div_small(p, vw, 1.0f / float(vw)), lx = p - ly * vw;
-          const int i = x0 + lx;
-          const int j = a.row0 + (y0 + ly) * a.row_step;
-          prng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(sbase + qs));
-          float ju, jv;
-          prng.pair(ju, jv);
-          const float u = (float(i) + ju) * cam_lds[19];  // main.cpp:278, by the reciprocal
-          const float vv = (float(j) + jv) * cam_lds[20];  // main.cpp:279
-          get_ray<true, float>(lds_camera(cam_lds), u, vv, prng, po, pd);
-        }
-        return true;
+        const int jj = int(old & kQJobMask), nq = Q.item[s2][6];
+        if (jj >= nq) continue;
+        slot = int(s2);
+        j0 = jj;
+        return min(want, nq - jj);
       }
       // handed out (or no item yet): fetch the next item into a free slot
       uint32_t won = 0;
@@ -1099,7 +1078,7 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
         if (q_uniform(q_load(reinterpret_cast<uint32_t *>(&Q.item[k][7]))) == 0) f = k;
       if (f < 0) {  // every slot still has paths in flight: retry later
         if (lane == 0) q_store(&Q.jobs, v);
-        return false;
+        return 0;
       }
       for (;;) {
         unsigned itn = 0;
@@ -1108,7 +1087,7 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
         if (int(itn) >= a.n_items) {
           if (lane == 0) q_store(&Q.jobs, kQDrained << kQJobBits);
           drained = true;
-          return false;
+          return 0;
         }
         const ItemDesc cd = describe_item<TW>(a, int(itn));
         if (cd.nq <= 0) continue;  // an empty item: nothing to render
@@ -1128,7 +1107,56 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
         break;
       }
     }
-    return false;
+    return 0;
+  };
+
+  // Camera rays straight into the pool: all 64 lanes make one each (with its
+  // big-sphere pass and bin key) and park it in a free slot, so a lane holds
+  // one ray at a time and generation runs with every lane busy.
+  auto generate = [&]() {
+    uint32_t hf = 0;
+    const int nf = claim(kQFree, 64, hf);
+    if (nf == 0) return;
+    int slot = 0, j0 = 0;
+    const int n = drained ? 0 : claim_jobs(nf, slot, j0);
+    const uint32_t fs = take(kQFree, hf + uint32_t(lane), lane < nf) & (kQSlots - 1);
+    int ring = -1;
+    if (lane < n) {
+      // job q -> pixel q % nv, sample q / nv (q < nq <= 64 * 65535 < 2^22: div_small is exact)
+      const int x0 = Q.item[slot][0], y0 = Q.item[slot][1], vw = Q.item[slot][2], nv = Q.item[slot][3];
+      const int sbase = Q.item[slot][4];
+      const int q = j0 + lane;
+      const int qs = div_small(q, nv, 1.0f / float(nv));
+      const int p = q - qs * nv;
+      const int ly = div_small(p, vw, 1.0f / float(vw)), lx = p - ly * vw;
+      const int i = x0 + lx;
+      const int j = a.row0 + (y0 + ly) * a.row_step;
+      Xoro g;
+      g.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(sbase + qs));
+      float ju, jv;
+      g.pair(ju, jv);
+      const float u = (float(i) + ju) * cam_lds[19];  // main.cpp:278, by the reciprocal
+      const float vv = (float(j) + jv) * cam_lds[20];  // main.cpp:279
+      V3<float> co, cd;
+      get_ray<true, float>(lds_camera(cam_lds), u, vv, g, co, cd);
+      float ct;
+      int cb;
+      grid_big<kBigGroup>(a.acc, co, cd, ct, cb
+#if RTMI_STATS
+                          , cnt.bvh_stats
+#endif
+      );
+      ring = min(grid_bound<FLAT>(co, cd, ct), kQBins - 1);
+      Q.ray[0][fs] = make_float4(co.x, co.y, co.z, 1.0f);
+      Q.ray[1][fs] = make_float4(cd.x, cd.y, cd.z, 1.0f);
+      Q.ray[2][fs] = make_float4(1.0f, ct, __int_as_float((slot << 30) | (p << 24)), __int_as_float(cb));
+      Q.ray[3][fs] = make_float4(__uint_as_float(uint32_t(g.s0)), __uint_as_float(uint32_t(g.s0 >> 32)),
+                                 __uint_as_float(uint32_t(g.s1)), __uint_as_float(uint32_t(g.s1 >> 32)));
+    } else if (lane < nf) {
+      ring = kQFree;  // a free slot not needed after all: back to the free ring
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    put(ring, fs, ring >= 0);
   };
 
   // An item slot whose paths have all ended: its sums to the output (the
@@ -1157,52 +1185,16 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
     if (lane == 0) q_store(reinterpret_cast<uint32_t *>(&Q.item[s][7]), 0u);
   };
 
-  auto pull = [](int src4, float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(src4, __float_as_int(v))); };
-  auto pull64 = [](int src4, uint64_t v) {
-    const uint32_t lo = uint32_t(__builtin_amdgcn_ds_bpermute(src4, int(uint32_t(v))));
-    const uint32_t hi = uint32_t(__builtin_amdgcn_ds_bpermute(src4, int(uint32_t(v >> 32))));
-    return (uint64_t(hi) << 32) | lo;
-  };
-
   uint32_t idle = 0;
-  for (;;) {
-    // 1. empty lanes take camera rays
-    unsigned long long empty = __ballot(!has);
-    while (empty) {
-      if (ppos >= pn && (drained || !refill())) break;
-      const int rank = q_rank(empty);
-      const int take_n = min(__popcll(empty), pn - ppos);
-      const int src4 = ((ppos + rank) & 63) << 2;
-      const V3<float> ro = mk(pull(src4, po.x), pull(src4, po.y), pull(src4, po.z));
-      const V3<float> rd = mk(pull(src4, pd.x), pull(src4, pd.y), pull(src4, pd.z));
-      Xoro g;
-      g.s0 = pull64(src4, prng.s0);
-      g.s1 = pull64(src4, prng.s1);
-      if (!has && rank < take_n) {
-        const int q = p_j0 + ((ppos + rank) & 63);
-        const int p = q - div_small(q, p_nv, 1.0f / float(p_nv)) * p_nv;
-        o = ro;
-        d = rd;
-        rng = g;
-        meta = (p_slot << 30) | (p << 24);
-        T = mk(1.f, 1.f, 1.f);
-        has = true;
-        prep = true;
-      }
-      ppos = __builtin_amdgcn_readfirstlane(ppos + take_n);
-      empty = __ballot(!has);
-    }
-    // 2. new rays (camera or scattered): the big spheres, then the bin key
-    if (prep) {
-      grid_big<kBigGroup>(a.acc, o, d, tmax, best
 #if RTMI_STATS
-                          , cnt.bvh_stats
+  unsigned npass = 0;
 #endif
-      );
-      key = min(grid_bound<FLAT>(o, d, tmax), kQBins - 1);
-      prep = false;
-    }
-    // 3. the exchange: the fullest bin's rays for the lanes not holding one
+  for (;;) {
+    // 1. camera rays into the pool while it has a batch of free slots
+    if (!drained && int(q_uniform(q_load(&Q.tail[kQFree]) - q_load(&Q.head[kQFree]))) >= 64) generate();
+    // 2. the exchange: the fullest bin's rays for the lanes not holding one of
+    // its rays (empty lanes first: an idle lane costs more than one holding
+    // another bin's ray); lanes left without a partner keep their ray
     {
       uint32_t c = 0;
       if (lane < kQBins) c = q_load(&Q.tail[lane]) - q_load(&Q.head[lane]);
@@ -1221,66 +1213,36 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
       const int nt = __popcll(tm);
       uint32_t h = 0;
       const int n = (tm | lm) && bc ? claim(bs, nt + __popcll(lm), h) : 0;
-      // empty lanes first (an idle lane costs more than one holding another bin's ray)
       const int rank = has ? nt + q_rank(lm) : q_rank(tm);
       const bool got = !keep && rank < n;
       const uint32_t slot = take(bs, h + uint32_t(rank), got) & (kQSlots - 1);
-      // leavers without a partner park their ray in a free slot (filling the pool)
-      const bool park_want = has && !keep && !got;
-      const unsigned long long pm = __ballot(park_want);
-      uint32_t hf = 0;
-      const int nf = pm ? claim(kQFree, __popcll(pm), hf) : 0;
-      const int prank = q_rank(pm);
-      const bool park = park_want && prank < nf;
-      const uint32_t fslot = take(kQFree, hf + uint32_t(prank), park) & (kQSlots - 1);
       int push_ring = -1;
-      uint32_t push_slot = 0;
       if (got) {
-        // quarter by quarter (one quarter of a second ray live at a time):
-        // read the slot's quarter, write the lane's own there, take the read one
+        const float4 r0 = Q.ray[0][slot], r1 = Q.ray[1][slot], r2 = Q.ray[2][slot], r3 = Q.ray[3][slot];
+        if (has) store_ray(slot);
         push_ring = has ? key : kQFree;
-        push_slot = slot;
-        const float4 r0 = Q.ray[0][slot];
-        if (has) Q.ray[0][slot] = make_float4(o.x, o.y, o.z, T.x);
         o = mk(r0.x, r0.y, r0.z);
-        T.x = r0.w;
-        const float4 r1 = Q.ray[1][slot];
-        if (has) Q.ray[1][slot] = make_float4(d.x, d.y, d.z, T.y);
         d = mk(r1.x, r1.y, r1.z);
-        T.y = r1.w;
-        const float4 r2 = Q.ray[2][slot];
-        if (has) Q.ray[2][slot] = make_float4(T.z, tmax, __int_as_float(meta), __int_as_float(best));
-        T.z = r2.x;
+        T = mk(r0.w, r1.w, r2.x);
         tmax = r2.y;
         meta = __float_as_int(r2.z);
         best = __float_as_int(r2.w);
-        const float4 r3 = Q.ray[3][slot];
-        if (has)
-          Q.ray[3][slot] = make_float4(__uint_as_float(uint32_t(rng.s0)), __uint_as_float(uint32_t(rng.s0 >> 32)),
-                                       __uint_as_float(uint32_t(rng.s1)), __uint_as_float(uint32_t(rng.s1 >> 32)));
         rng.s0 = (uint64_t(__float_as_uint(r3.y)) << 32) | __float_as_uint(r3.x);
         rng.s1 = (uint64_t(__float_as_uint(r3.w)) << 32) | __float_as_uint(r3.z);
         has = true;
       }
-      if (park) {
-        store_ray(fslot);
-        push_ring = key;
-        push_slot = fslot;
-        has = false;
-      }
       // the ray writes (and the reads of swapped-out slots) before the pushes
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      for (int r = 0; r < kQRings; ++r)
-        if (__ballot(push_ring == r)) put(r, push_slot, push_ring == r);
+      put(push_ring, slot, push_ring >= 0);
     }
     const unsigned long long live = __ballot(has);
     if (live == 0) ++idle;
     if (__ballot(fault) || idle > kQIdleMax) {
-      if (lane == 0) atomicOr(&segments[7], 1ull << 63);  // watchdog: the host reports RT_EHIP
+      if (lane == 0) atomicOr(&segments[7], 1ull << 63);  // watchdog
       break;
     }
     if (live == 0) {
-      if (drained && ppos >= pn) {
+      if (drained) {
         uint32_t c = 0;
         if (lane < kQBins) c = q_load(&Q.tail[lane]) - q_load(&Q.head[lane]);
         if (__ballot(c != 0) == 0) break;  // no rays left anywhere this wave could take
@@ -1290,11 +1252,16 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
     }
     idle = 0;
     nseg = unsigned(__builtin_amdgcn_readfirstlane(int(nseg + unsigned(__popcll(live)))));
-    // 4. one segment of every held ray, from its big-sphere result
+#if RTMI_STATS
+    ++npass;
+#endif
+    // 3. one segment of every held ray, from its big-sphere result
     bool done = false;
     V3<float> col = mk(0.f, 0.f, 0.f);
     if (has) done = path_segment<ACC, true>(sc, nullptr, a, o, d, T, meta, rng, col, cnt, segments, tmax, best);
-    // 5. ended paths: colour to their item's sums; the item's last path flushes it
+    // 4. ended paths: colour to their item's sums; the item's last path
+    // flushes it.  Survivors: the big spheres and the bin key of their next
+    // segment.
     int cs = 0;
     if (done) {
       cs = int(uint32_t(meta) >> 30);
@@ -1305,7 +1272,12 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
       q_add(&Q.segs[cs], uint32_t(meta & 0xFFFFFF) + 1u);
       has = false;
     } else if (has) {
-      prep = true;
+      grid_big<kBigGroup>(a.acc, o, d, tmax, best
+#if RTMI_STATS
+                          , cnt.bvh_stats
+#endif
+      );
+      key = min(grid_bound<FLAT>(o, d, tmax), kQBins - 1);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the sums before the count
     bool complete = false;
@@ -1314,6 +1286,9 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
       flush(__builtin_amdgcn_readlane(cs, int(__builtin_ctzll(cm))));
   }
   if (lane == 0) atomicAdd(segments, (unsigned long long)nseg);
+#if RTMI_STATS
+  if (lane == 0) atomicAdd(&segments[7], (unsigned long long)npass);  // wave passes with a live lane
+#endif
   flush_counters(cnt, lane, segments);
 }
 
@@ -2231,7 +2206,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   a.block_flush = !persistent && !queue && nch1 % grid_wpb == 0 && nch2 % grid_wpb == 0 && ctx->block_flush;
   a.block_owns_tile = a.block_flush && !pass_accum && nch1 == grid_wpb && nch2 == 0 && ctx->block_owns;
   // the queue kernel: an item that covers all its tile's samples writes the floats
-  if (queue) a.block_owns_tile = !pass_accum && nch1 == 1 && nch2 == 0 && ctx->block_owns;
+  if (queue) a.block_owns_tile = !pass_accum && nch1 == 1 && nch2 == 0;
   const bool chunked = pass_accum || nch1 + nch2 > 1;
   if (!ctx->probing) {
     const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush + a.block_owns_tile, persistent ? 0 : 1,

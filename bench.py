@@ -253,12 +253,14 @@ def executed_counts_child(argv):
 
     Wc, Hc, S, row0, row_step, nrows = (int(x) for x in argv[:6])
     accel = argv[6]
+    kernel = argv[7] if len(argv) > 7 else "auto"
     L = rt.load()
     L.rt_ctx_debug_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     L.rt_ctx_debug_counters.restype = C.c_int
     world = rt.random_scene()
     r = rt.Renderer(world, 0)
     r.set_accel(accel)
+    r.set_kernel(kernel)
     strip = torch.empty((nrows, Wc, 3), dtype=torch.float32, device="cuda:0")
     r.render_rows(rt.final_camera(Wc / Hc), Wc, Hc, S, DEPTH, SEED, row0, row_step, nrows, strip.data_ptr(), 0)
     r.synchronize()
@@ -266,19 +268,20 @@ def executed_counts_child(argv):
     rt.check(L.rt_ctx_debug_counters(r._h, v), "rt_ctx_debug_counters")
     nbig, nnodes = r.accel_info()
     print(json.dumps({"segments": v[0], "node_visits": v[5], "leaf_sphere_tests": v[6], "node_iterations_wave": v[1],
-                      "leaf_sphere_iterations_wave": v[2], "root_resolutions_wave": v[4], "big_spheres": nbig,
+                      "leaf_sphere_iterations_wave": v[2], "root_resolutions_wave": v[4],
+                      "wave_passes": v[7] & ((1 << 63) - 1), "big_spheres": nbig,
                       "bvh_nodes": nnodes, "checksum": float(strip.double().sum().item())}), flush=True)
     r.close()
 
 
-def executed_counts(Wc, Hc, S, row0, row_step, nrows, accel="bvh"):
-    """Run the RTMI_STATS build on the same rows in a child process."""
+def executed_counts(Wc, Hc, S, row0, row_step, nrows, accel="bvh", kernel="auto"):
+    """Run the RTMI_STATS build on the same rows (same kernel) in a child process."""
     if not os.path.exists(STATS_LIB):
         return None, f"{STATS_LIB} not built"
     env = dict(os.environ, RTMI_LIBRARY=STATS_LIB)
     try:
         out = subprocess.run([sys.executable, os.path.abspath(__file__), "--exec-counts", str(Wc), str(Hc), str(S),
-                              str(row0), str(row_step), str(nrows), accel],
+                              str(row0), str(row_step), str(nrows), accel, kernel],
                              capture_output=True, text=True, timeout=240, env=env, check=True).stdout
         return json.loads(out.strip().splitlines()[-1]), None
     except Exception as e:  # reported, never replaced by another figure
@@ -723,7 +726,7 @@ def main():
         elif args.no_exec_counts or STUB:
             flop_exec, why = None, "skipped (stub renderer)" if STUB else "skipped (--no-exec-counts)"
         else:
-            counts, why = executed_counts(W, H, SPP, row0, row_step, nrows, args.accel)
+            counts, why = executed_counts(W, H, SPP, row0, row_step, nrows, args.accel, args.kernel)
             flop_exec = executed_flop(counts, args.accel) if counts else None
             if counts and counts["segments"] != segs:
                 why = f"stats build segments {counts['segments']} != product {segs}"
@@ -775,6 +778,8 @@ def main():
                 "walk_lane_utilisation": round(counts["node_visits"] / max(1, 64 * counts["node_iterations_wave"]), 4),
                 "leaf_lane_utilisation": round(counts["leaf_sphere_tests"] / max(1, 64 * counts["leaf_sphere_iterations_wave"]), 4),
             }
+            if counts.get("wave_passes"):  # the queue kernel's stats build counts its wave passes
+                roof["counts"]["live_lanes_per_pass"] = round(counts["segments"] / counts["wave_passes"], 2)
         # Context beside the algorithmic fraction, from the committed PMC passes
         # of the same kernel on the same workload (tools/profile.sh,
         # profiles/pmc_valu.json) over this run's kernel time: every FP32 FLOP

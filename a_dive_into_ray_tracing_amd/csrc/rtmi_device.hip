@@ -873,7 +873,8 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
 // 512-ray pool).  No wave waits for another: bins are multi-producer /
 // multi-consumer rings of slot indices in LDS (a claim by compare-and-swap on
 // the ring head, a push by atomic add on its tail, entries polled until
-// written), so the only coupling is the pool.  Camera jobs come from block
+// written), so the only coupling is the pool.  All of it lives in LDS, so the
+// fences order LDS only (s_waitcnt lgkmcnt(0), no wait on global memory).  Camera jobs come from block
 // work items (tile, sample range) held in kQItems LDS slots with their
 // fixed-point sums: a ray carries its item slot and pixel, whichever wave ends
 // the path adds its colour there, and the wave that ends an item's last path
@@ -881,6 +882,9 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
 // other kernel's, in any order of rays and waves.
 #ifndef RTMI_QUEUE_BINS
 #define RTMI_QUEUE_BINS 8
+#endif
+#ifndef RTMI_QUEUE_PHASES
+#define RTMI_QUEUE_PHASES 0
 #endif
 #ifndef RTMI_QUEUE_SLOTS
 #define RTMI_QUEUE_SLOTS 512
@@ -1049,7 +1053,7 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
   auto claim_jobs = [&](int want, int &slot, int &j0) {
     for (int attempt = 0; attempt < 8; ++attempt) {
       const uint32_t v = q_uniform(q_load(&Q.jobs));
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the item fields after the word naming them
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");  // the item fields after the word naming them
       const uint32_t s = v >> kQJobBits;
       if (s == kQDrained) {
         drained = true;
@@ -1062,7 +1066,7 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
         old = q_uniform(old);
         const uint32_t s2 = old >> kQJobBits;
         if (s2 >= kQItems) continue;  // the word changed state meanwhile (this add is overwritten)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
         const int jj = int(old & kQJobMask), nq = Q.item[s2][6];
         if (jj >= nq) continue;
         slot = int(s2);
@@ -1102,7 +1106,7 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
           Q.done[f] = 0;
           Q.segs[f] = 0;
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         if (lane == 0) q_store(&Q.jobs, uint32_t(f) << kQJobBits);
         break;
       }
@@ -1155,7 +1159,7 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
     } else if (lane < nf) {
       ring = kQFree;  // a free slot not needed after all: back to the free ring
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     put(ring, fs, ring >= 0);
   };
 
@@ -1163,7 +1167,7 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
   // floats when the item covers every sample of its tile, else the global
   // fixed-point accumulator), its cost to the tile's, then the slot is free.
   auto flush = [&](int s) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     const int x0 = Q.item[s][0], y0 = Q.item[s][1], vw = Q.item[s][2], nv = Q.item[s][3], tile = Q.item[s][5];
     unsigned long long v[3];
 #pragma unroll
@@ -1181,7 +1185,7 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
       }
     }
     if (lane == 0 && a.tile_cost) atomicAdd(&a.tile_cost[tile], q_load(&Q.segs[s]));
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     if (lane == 0) q_store(reinterpret_cast<uint32_t *>(&Q.item[s][7]), 0u);
   };
 
@@ -1189,9 +1193,19 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
 #if RTMI_STATS
   unsigned npass = 0;
 #endif
+#if RTMI_QUEUE_PHASES
+  // analysis build: wave cycles (s_memtime) of generation, exchange, idle
+  // passes, segment, end-of-segment work -> segments[1..5]
+  unsigned long long qc[5] = {0, 0, 0, 0, 0};
+#define QPH(k) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); qc[k] += t_ - qt; qt = t_; }
+  unsigned long long qt = __builtin_amdgcn_s_memtime();
+#else
+#define QPH(k)
+#endif
   for (;;) {
     // 1. camera rays into the pool while it has a batch of free slots
     if (!drained && int(q_uniform(q_load(&Q.tail[kQFree]) - q_load(&Q.head[kQFree]))) >= 64) generate();
+    QPH(0)
     // 2. the exchange: the fullest bin's rays for the lanes not holding one of
     // its rays (empty lanes first: an idle lane costs more than one holding
     // another bin's ray); lanes left without a partner keep their ray
@@ -1232,13 +1246,14 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
         has = true;
       }
       // the ray writes (and the reads of swapped-out slots) before the pushes
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
       put(push_ring, slot, push_ring >= 0);
     }
+    QPH(1)
     const unsigned long long live = __ballot(has);
     if (live == 0) ++idle;
     if (__ballot(fault) || idle > kQIdleMax) {
-      if (lane == 0) atomicOr(&segments[7], 1ull << 63);  // watchdog
+      if (lane == 0) atomicOr(&segments[7], 1ull << 63);  // watchdog: rt_render / rt_ctx_synchronize report RT_EHIP
       break;
     }
     if (live == 0) {
@@ -1248,6 +1263,7 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
         if (__ballot(c != 0) == 0) break;  // no rays left anywhere this wave could take
       }
       __builtin_amdgcn_s_sleep(4);
+      QPH(2)
       continue;
     }
     idle = 0;
@@ -1259,6 +1275,7 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
     bool done = false;
     V3<float> col = mk(0.f, 0.f, 0.f);
     if (has) done = path_segment<ACC, true>(sc, nullptr, a, o, d, T, meta, rng, col, cnt, segments, tmax, best);
+    QPH(3)
     // 4. ended paths: colour to their item's sums; the item's last path
     // flushes it.  Survivors: the big spheres and the bin key of their next
     // segment.
@@ -1279,12 +1296,18 @@ __global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
       );
       key = min(grid_bound<FLAT>(o, d, tmax), kQBins - 1);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the sums before the count
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // the sums before the count
     bool complete = false;
     if (done) complete = int(q_add(&Q.done[cs], 1u)) + 1 == Q.item[cs][6];
     for (unsigned long long cm = __ballot(complete); cm; cm &= cm - 1)
       flush(__builtin_amdgcn_readlane(cs, int(__builtin_ctzll(cm))));
+    QPH(4)
   }
+#if RTMI_QUEUE_PHASES
+  if (lane == 0)
+    for (int k = 0; k < 5; ++k) atomicAdd(&segments[1 + k], qc[k]);
+#endif
+#undef QPH
   if (lane == 0) atomicAdd(segments, (unsigned long long)nseg);
 #if RTMI_STATS
   if (lane == 0) atomicAdd(&segments[7], (unsigned long long)npass);  // wave passes with a live lane
@@ -2518,11 +2541,25 @@ RTMI_EXPORT int rt_accum_load(rt_ctx *ctx, const char *path, const rt_scene *sce
   return RT_OK;
 }
 
+namespace {
+// After a queue-kernel launch has finished: its watchdog (a ring entry or an
+// idle loop that waited far past any legitimate delay) marks segments[7]
+// bit 63 and the kernel leaves early — the image is then incomplete.
+int check_queue_fault(rt_ctx *ctx, hipStream_t st) {
+  if (ctx->last_sched[6] != 2) return RT_OK;
+  unsigned long long v = 0;
+  HIP_TRY(hipMemcpyAsync(&v, ctx->segments + 7, sizeof v, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (v >> 63) return set_error(RT_EHIP, "queue kernel watchdog fired: the render is incomplete");
+  return RT_OK;
+}
+}  // namespace
+
 RTMI_EXPORT int rt_ctx_synchronize(rt_ctx *ctx) {
   if (!ctx) return set_error(RT_EINVAL, "null ctx");
   DeviceGuard guard(ctx->device);
   HIP_TRY(hipStreamSynchronize(ctx->stream));
-  return RT_OK;
+  return check_queue_fault(ctx, ctx->last_stream ? ctx->last_stream : ctx->stream);
 }
 
 RTMI_EXPORT int rt_render(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t spp, int32_t max_depth,
@@ -2539,7 +2576,7 @@ RTMI_EXPORT int rt_render(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t 
   if ((rc = render_rows_impl(ctx, cam, W, H, spp, max_depth, seed, 0, 1, H, ctx->scratch, ctx->stream))) return rc;
   HIP_TRY(hipMemcpyAsync(sum, ctx->scratch, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
-  return RT_OK;
+  return check_queue_fault(ctx, ctx->stream);
 }
 
 RTMI_EXPORT int rt_replay_worker(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t spp,

@@ -75,7 +75,7 @@ struct RenderArgs {
   // progressive passes: this launch renders samples s_base + [0, spp)
   int32_t s_base;
   uint64_t out_elems;  // elements of accum / out (RTMI_CHECK builds verify every write)
-  Accel acc;           // BVH kernels only (DESIGN.md §4.4)
+  Accel acc;           // BVH kernels only (DESIGN.md §4.3)
   // cost-ordered dispatch: tile rank -> tile (null: identity)
   // and per-tile world.hit counts of this launch (null: not measured)
   const int32_t *tile_order;
@@ -185,8 +185,9 @@ template <bool BVH> struct GridShape {
 };
 // The persistent kernel runs brute-force scenes only: with the BVH or the
 // grid it measured slower than the grid kernel everywhere (round 2: config 2
-// frame / 1/8 strip 30.9 / 4.72 ms against 26.0 / 3.70, profiles/r02/ab_persistent/),
-// so RT_KERNEL_PERSISTENT with an accelerator runs the grid kernel.
+// frame / 1/8 strip 30.9 / 4.72 ms against 26.0 / 3.70; profiles/README.md),
+// so RT_KERNEL_PERSISTENT with an accelerator runs the grid kernel.  (The
+// CU-resident design of round 5, render_queue, is RT_KERNEL_QUEUE.)
 
 // The camera and the reciprocals of main.cpp:278-279's (W-1, H-1)
 // denominators in LDS (21 floats), read at each regeneration instead of held
@@ -467,7 +468,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
     }
   };
 
-  // Camera-ray pool (DESIGN.md §4.6): lane L holds the camera ray of job
+  // Camera-ray pool (DESIGN.md §4.5): lane L holds the camera ray of job
   // pbase + L, generated by all 64 lanes at once; a lane whose path ended
   // takes the next unused slot through ds_bpermute.  The ray generation runs
   // with every lane busy, once per 64 jobs, instead of once per loop pass
@@ -860,7 +861,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
 
 // ---------------------------------------------------------------------------
 // queue kernel: CU-resident 16-wave blocks sharing one LDS pool of rays,
-// binned by the pre-walk bound (DESIGN.md §4.7)
+// binned by the pre-walk bound (DESIGN.md §4.6)
 // ---------------------------------------------------------------------------
 // The grid kernel's waves each walk their own 64 paths: a wave pays for its
 // longest walk, so the walk runs at 0.34 lane utilisation.  Here a block's
@@ -1451,7 +1452,7 @@ struct rt_ctx {
   int32_t cu_count = 0;                    // compute units of the device
   int32_t queue_blocks = 0;                // resident render_queue blocks for queue_lds dynamic LDS bytes
   size_t queue_lds = 0;
-  // BVH (DESIGN.md §4.4), built by rt_ctx_set_scene
+  // BVH (DESIGN.md §4.3), built by rt_ctx_set_scene
   int32_t accel = RT_ACCEL_GRID;  // the fastest structure (brute force when the scene has none)
   SpherePair *big_pairs = nullptr;
   int32_t *big_idx = nullptr;
@@ -1461,7 +1462,7 @@ struct rt_ctx {
   float4 *bvh_sph = nullptr;
   int32_t *bvh_idx = nullptr;
   int32_t nbvh_sph = 0;
-  // uniform grid (DESIGN.md §4.5), built by rt_ctx_set_scene beside the BVH
+  // uniform grid (DESIGN.md §4.4), built by rt_ctx_set_scene beside the BVH
   float4 *grid_sph = nullptr;  // every sphere by scene index
   uint32_t *grid_cells = nullptr;  // ncells + 1: each cell's first reference
   uint32_t *grid_refs = nullptr;   // 16 x scene index (byte offsets into the LDS sphere array)
@@ -1617,7 +1618,7 @@ RTMI_EXPORT int rt_ctx_destroy(rt_ctx *ctx) {
 }
 
 namespace {
-constexpr size_t kBvhLdsMax = 64 * 1024;  // BVH bytes staged per block (DESIGN.md §4.4)
+constexpr size_t kBvhLdsMax = 64 * 1024;  // BVH bytes staged per block (DESIGN.md §4.3)
 
 // BVH over the small spheres: binary, SAH split (full sweep of the sorted
 // centroids on each axis: the split minimising area(L)*|L| + area(R)*|R|),
@@ -1724,7 +1725,7 @@ struct BvhBuilder {
 }  // namespace
 
 namespace {
-// Uniform grid over the small spheres (DESIGN.md §4.5).  The box of their
+// Uniform grid over the small spheres (DESIGN.md §4.4).  The box of their
 // margin-grown boxes (the BVH's margins) is cut into cells of about
 // RTMI_GRID_CELLS (default 0.3) cells per sphere, as near cubic as the box
 // allows (the final scene's thin layer of spheres: 30 x 1 x 30 cells); every
@@ -1742,7 +1743,8 @@ bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, int32_t 
   if (n > 65535) return false;  // references are 16-bit scene indices
   const char *env = std::getenv("RTMI_GRID_CELLS");
   // 0.3 cells per sphere: config 2 33.3 ms (0.2: 33.3, 0.5: 33.6, 1: 34.5,
-  // 2: 35.2, 4: 38.0; profiles/r02/grid_sweep)
+  // 2: 35.2, 4: 38.0; round 2) and, on the record slots, 19.30 ms (0.2:
+  // 19.38, 0.25: 19.33, 0.4: 19.33; profiles/r04/grid_density.txt)
   const double per_sphere = env && std::atof(env) > 0 ? std::atof(env) : 0.3;
   double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
   for (int32_t k : small) {
@@ -1944,7 +1946,7 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
     // offered (RT_ACCEL_BVH renders brute force)
     const size_t lds = bvh_lds_bytes(int32_t(b.nodes.size()), int32_t(b.sph.size()));
     ctx->nnodes = lds <= kBvhLdsMax && n <= 65535 ? int32_t(b.nodes.size()) : 0;
-    // uniform grid over the same small spheres (DESIGN.md §4.5)
+    // uniform grid over the same small spheres (DESIGN.md §4.4)
     ctx->grid_ok = false;
     GridBuild gb;
     if (!small.empty() && build_grid(b, small, n, nb_pad, gb)) {
@@ -2158,7 +2160,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
                            ? 1
                            : (ctx->accel == RT_ACCEL_GRID && ctx->grid_ok ? (ctx->grid.n[1] == 1 ? 3 : 2) : 0);
   const bool bvh = acc_kind != 0;
-  // the queue kernel (DESIGN.md §4.7): grid scenes, when selected
+  // the queue kernel (DESIGN.md §4.6): grid scenes, when selected
   const bool queue = acc_kind >= 2 && ctx->kernel == RT_KERNEL_QUEUE && TW <= 16;
   const int64_t qblocks = queue ? queue_resident_blocks(ctx, accel_lds_bytes(accel_of(ctx, acc_kind), acc_kind)) : 0;
   // the persistent kernel runs brute-force scenes only (see the note above stage_camera)

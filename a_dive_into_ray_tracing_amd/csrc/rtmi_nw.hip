@@ -120,7 +120,7 @@ __device__ __forceinline__ int64_t fixed(float c) {
 // The camera, shutter and image size in LDS (23 floats), read at each
 // regeneration: the kernel's scalar registers otherwise overflow and the
 // compiler parks them in VGPR lanes (v_readlane at every regeneration), as in
-// the RTIOW kernel (DESIGN.md §4.6).  Staged before stage_scene's barrier.
+// the RTIOW kernel (DESIGN.md §4.5).  Staged before stage_scene's barrier.
 __device__ __forceinline__ void stage_camera(float *cl, const Args &a) {
   const unsigned t = threadIdx.x;
   if (t < 23) {
@@ -457,7 +457,7 @@ struct rt_nw_ctx {
   Image *imgd = nullptr;
   float4 *nodes = nullptr;  // 2 * nnodes: lo[] then hi[]
   int32_t nobj = 0, nnodes = 0, ninst = 0, nmat = 0, ntex = 0;
-  // uniform grid (DESIGN.md §9.5): descriptor, global arrays, brute-force list
+  // uniform grid (DESIGN.md §9): descriptor, global arrays, brute-force list
   bool grid_ok = false;
   NwGridDesc grid{};
   int32_t grid_max_cell = 0;

@@ -21,7 +21,7 @@ struct Node {
 };
 
 // What the device renders: flattened records in BVH leaf order, plus each
-// object's world-insertion index (the tie-break key, DESIGN.md §9.2).
+// object's world-insertion index (the tie-break key, DESIGN.md §9).
 struct DeviceScene {
   std::vector<Obj> obj;          // non-media objects, BVH leaf order; aux = twin medium's index in med + 1
   std::vector<int32_t> obj_id;   // insertion index of obj[k]
@@ -37,7 +37,7 @@ struct DeviceScene {
   std::vector<Node> nodes;
   float background[3];
   bool has_media;
-  // uniform grid over the same objects (DESIGN.md §9.5); grid_ok false when
+  // uniform grid over the same objects (DESIGN.md §9); grid_ok false when
   // the scene has none (no small objects, or it would not fit in LDS)
   bool grid_ok = false;
   float grid_g0[3], grid_h[3], grid_inv_h[3], grid_g1[3];

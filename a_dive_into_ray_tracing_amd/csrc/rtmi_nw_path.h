@@ -4,7 +4,7 @@
 // operation for operation by the CPU oracle (oracle/rt_nw_oracle.c), so the
 // kernel's images equal the oracle's bit for bit.  Transcendentals (sin,
 // log, atan2, acos) are our own polynomial evaluations for the same reason.
-// Semantics and deviations: DESIGN.md §9.2.
+// Semantics and deviations: DESIGN.md §9.
 #pragma once
 
 #include "rtmi_nw_types.h"
@@ -103,7 +103,7 @@ __device__ __forceinline__ float nw_acosf(float x) {
 // ---------------------------------------------------------------------------
 // scene view
 // ---------------------------------------------------------------------------
-// The Next-Week grid's descriptor (DESIGN.md §9.5): cell c lists
+// The Next-Week grid's descriptor (DESIGN.md §9): cell c lists
 // refs[cell_start[c]] .. refs[cell_start[c+1]] (16-bit leaf-order slots).
 struct NwGridDesc {
   float g0[3], h[3], inv_h[3], g1[3];  // origin, cell size, 1/h, far corner
@@ -130,7 +130,7 @@ struct View {
   int32_t nnodes;
   float bg[3];
   int32_t has_media;
-  // uniform grid over the objects (RT_NW_ACCEL_GRID, DESIGN.md §9.5): its
+  // uniform grid over the objects (RT_NW_ACCEL_GRID, DESIGN.md §9): its
   // descriptor (cell_start / refs: global copies) and the objects tested
   // brute force beside it (leaf-order slots)
   NwGridDesc grid;
@@ -403,7 +403,7 @@ __device__ __forceinline__ bool hit_object(const View &sc, const DevObj &ob, V o
   }
 }
 
-// Closest hit of a segment (DESIGN.md §9.2).  1. Media, in insertion order:
+// Closest hit of a segment (DESIGN.md §9).  1. Media, in insertion order:
 // each one that hits is a candidate and sets its bit in the mask.  2. The
 // object BVH (global memory, stackless skip-link walk, slab test clipped to
 // [0, best_t]); an object whose twin medium hit is skipped.  The winner is
@@ -502,7 +502,7 @@ __host__ __device__ constexpr size_t nw_grid_lds_bytes(int32_t nobj, int32_t nce
 // cells the ray crosses inside [0, best_t], testing each cell's objects with
 // hit_object and the same order-independent (t, insertion index) rule.  The
 // walk stops at the first cell whose exit is at or beyond the closest hit so
-// far.  Exact for the reasons of the RTIOW grid (DESIGN.md §4.5): an
+// far.  Exact for the reasons of the RTIOW grid (DESIGN.md §4.4): an
 // object's hit point — world ray at its t, up to the float error of an
 // instance transform — lies inside its box grown by its margin (>= 1e-3 of
 // its coordinate scale), so inside a cell that lists it; an object listed in

@@ -348,7 +348,7 @@ int flatten(rt_nw_scene *s) {
 // every box on its path, as a median split leaves it.  Leaves of <=
 // kNodeLeafMax objects, DFS order with skip links.  Boxes are the objects'
 // double bounds, each grown by its own margin, rounded outward to float
-// (the RTIOW BVH's margin argument, DESIGN.md §4.4).
+// (the RTIOW BVH's margin argument, DESIGN.md §4.3).
 struct ObjBvh {
   const std::vector<Bounds> &b;
   const std::vector<double> &w;  // per-object test cost (relative)
@@ -437,7 +437,7 @@ struct ObjBvh {
   }
 };
 
-// Uniform grid over the non-media objects (DESIGN.md §9.5), the RTIOW grid's
+// Uniform grid over the non-media objects (DESIGN.md §9), the RTIOW grid's
 // build (rtmi_device.hip build_grid) for general objects: an object whose box
 // is more than 8x the median's largest extent (the R = 1000 ground, a
 // room-sized light) is tested brute force beside the grid; the others are
@@ -536,7 +536,7 @@ int build_device_scene(rt_nw_scene *s, DeviceScene &out) {
   if (int rc = flatten(s)) return rc;
   const int n_all = int(s->flat_obj.size());
   if (n_all == 0) return set_error(RT_EINVAL, "rt_nw: empty world (rt_nw_world_add)");
-  // media are evaluated per segment before the BVH walk (DESIGN.md §9.2);
+  // media are evaluated per segment before the BVH walk (DESIGN.md §9);
   // the BVH holds the other objects
   std::vector<int32_t> med_index(n_all, -1), ids;
   out.med.clear();
@@ -566,7 +566,7 @@ int build_device_scene(rt_nw_scene *s, DeviceScene &out) {
     const Obj &o = s->flat_obj[k];
     cost[k] = (o.kind == kBox ? 3.0 : o.kind == kMovingSphere ? 1.2 : 1.0) + (o.inst >= 0 ? 0.3 : 0.0);
   }
-  // box margins (the RTIOW BVH's argument, DESIGN.md §4.4): 1e-3 of the
+  // box margins (the RTIOW BVH's argument, DESIGN.md §4.3): 1e-3 of the
   // object's own coordinate scale — ~100x the float error of its hit test —
   // plus 1e-6 of the scene's, for rays from far away.  One scene-wide margin
   // of 1e-3 of the scene scale grew every small box by ~2 units next to the

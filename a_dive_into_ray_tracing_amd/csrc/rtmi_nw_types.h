@@ -1,6 +1,6 @@
 // rtmi_nw_types.h — flattened Next-Week scene records, shared by the host
 // scene builder (rtmi_nw_scene.cpp) and the gfx950 kernels (rtmi_nw.hip).
-// Layout and semantics: DESIGN.md §9.1.  Not installed.
+// Layout and semantics: DESIGN.md §9.  Not installed.
 #pragma once
 
 #include <cstdint>
@@ -17,7 +17,7 @@ enum ObjKind : int32_t {
   kRectYZ = 4,        //          yz_rect    g0 = {y0, y1, z0, z1}, g1.x = k
   kBox = 5,           // box.h               g0 = {p0, 0}, g1 = {p1, 0}
   kMedium = 6,        // constant_medium.h   boundary geometry as its kind (aux & 255), g2.w = -1/density,
-                      //                     aux >> 8 = scattering-distance samples (DESIGN.md §9.2)
+                      //                     aux >> 8 = scattering-distance samples (DESIGN.md §9)
 };
 
 // material kinds = RT_NW_* (rtmi_nw.h)

@@ -40,7 +40,7 @@ template <bool F> __device__ __forceinline__ double madd(double a, double b, dou
 // compiler's IEEE lowering (~16 and ~10 VALU: denormal scaling, class checks,
 // v_div_scale / v_div_fmas / v_div_fixup), bit-identical to it for EVERY one
 // of the 2^32 inputs (rt_debug_exact_math checks all of them on the GPU:
-// tests/test_gpu_parity.py::test_exact_math_exhaustive; DESIGN.md §4.6).
+// tests/test_gpu_parity.py::test_exact_math_exhaustive; DESIGN.md §4.5).
 //  sqrt: the hardware v_sqrt_f32 (within 1 ulp), then the neighbour below or
 //  above when the exact residual x - s'*s says the true root lies past the
 //  midpoint (+inf passes through: its residuals are NaN); inputs below 2^-96
@@ -50,7 +50,7 @@ template <bool F> __device__ __forceinline__ double madd(double a, double b, dou
 //  division (a branch no realistic scene takes).
 // (The out-of-range inputs take the IEEE form behind a wave-uniform branch on
 // their ballot: the common path pays one compare and a scalar branch, not an
-// exec-mask save/restore — DESIGN.md §4.6.)
+// exec-mask save/restore — DESIGN.md §4.5.)
 __device__ __forceinline__ float sqrt_cr(float x) {
   // below 2^-96 (zero, denormals — which v_sqrt_f32 flushes — negatives,
   // NaN) the residuals would underflow: the IEEE lowering
@@ -403,7 +403,7 @@ __device__ __forceinline__ int32_t hit_world_packed(const SpherePair *__restrict
 }
 
 // ---------------------------------------------------------------------------
-// BVH over the small spheres (SURVEY §8(f) rank 3; DESIGN.md §4.4)
+// BVH over the small spheres (SURVEY §8(f) rank 3; DESIGN.md §4.3)
 // ---------------------------------------------------------------------------
 // Same hit as hit_world_packed, bit for bit: the same expanded per-sphere
 // arithmetic and root logic, and the reference's "later object wins ties"
@@ -438,7 +438,7 @@ constexpr int kLeafMax = RTMI_BVH_LEAF;
 constexpr int kBigGroup = RTMI_BIG_GROUP;  // sphere pairs per step of the big-sphere loop
 static_assert(kLeafMax >= 1 && kLeafMax <= 15, "leaf size");
 
-// Uniform grid over the small spheres (RT_ACCEL_GRID; DESIGN.md §4.5): cells
+// Uniform grid over the small spheres (RT_ACCEL_GRID; DESIGN.md §4.4): cells
 // of size h over the box g0 + [0, n*h) of the spheres' margin-grown boxes.
 // Cell c lists refs[cells[c] .. cells[c+1]): every sphere whose grown box
 // overlaps it, as 16 x its scene index.  In LDS (stage_grid) each reference
@@ -707,7 +707,7 @@ __device__ __forceinline__ void hit_big(const Accel &acc_s, V3<float> d, float K
 // index and its record) with exactly the brute-force arithmetic and the
 // order-independent tie rule.  (Measured and not kept: cells padded to
 // records of four references tested unrolled — more VALU work per cell.)  The walk stops at the first cell whose exit
-// lies at or beyond the closest hit so far.  Exact (DESIGN.md §4.5): every
+// lies at or beyond the closest hit so far.  Exact (DESIGN.md §4.4): every
 // sphere is listed in every cell its grown box overlaps, the grow margin
 // (>= 1e-3 of the sphere's scale) is orders of magnitude above the float
 // error of the cell boundaries (each computed directly from the cell index,
@@ -715,9 +715,9 @@ __device__ __forceinline__ void hit_big(const Accel &acc_s, V3<float> d, float K
 // lists that sphere; a sphere tested in several cells gives the same root
 // each time.  FLAT_Y: the grid has one cell layer in y (the final scene's
 // 20 x 1 x 20) — the same walk with the y axis' stepping state dropped: a y
-// face only ends the walk (5 VGPRs fewer in the loop; DESIGN.md §4.5).
+// face only ends the walk (5 VGPRs fewer in the loop; DESIGN.md §4.4).
 //
-// FROM_BIG (the queue kernel, DESIGN.md §4.7): the big spheres' pass was run
+// FROM_BIG (the queue kernel, DESIGN.md §4.6): the big spheres' pass was run
 // when the ray was made (grid_big): the walk starts from its result, given in
 // t_max0 / best0.
 template <int GP, bool FLAT_Y = false, bool FROM_BIG = false>
@@ -916,7 +916,7 @@ __device__ __forceinline__ void grid_big(const Accel &acc_s, V3<float> o, V3<flo
               );
 }
 
-// The queue kernel's bin key (DESIGN.md §4.7): an upper bound on the cells
+// The queue kernel's bin key (DESIGN.md §4.6): an upper bound on the cells
 // the walk will visit, known before it — the ray clipped to the grid box and
 // to the big spheres' t_max, then |dcx| + |dcy| + |dcz| + 1 between its entry
 // and exit cells (0: no cell to walk).  An ordering key only: any value

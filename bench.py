@@ -859,7 +859,7 @@ def main():
 
 NW_PUBLISHED_MSPS = 1200 * 800 * 500 / 37.8792 / 1e6  # rt_next_week/cuda/README.md:167-174 (RTX 2060 Max-Q)
 # Algorithmic FLOP of one miss test per Next-Week object kind (the reference's
-# hit functions; DESIGN.md §9.4): sphere.h 18 (as the RTIOW count, |d|^2
+# hit functions; DESIGN.md §9): sphere.h 18 (as the RTIOW count, |d|^2
 # hoisted); moving_sphere.h center(t) 12 + 18; aarect.h t, two coordinates 6;
 # box.h = its six rects 36; constant_medium.h its boundary twice + 4; and per
 # instance (translate + rotate_y of the ray) 15.

@@ -135,12 +135,12 @@ int rt_ctx_set_schedule(rt_ctx *ctx, int32_t chunk, int32_t tail_spp, int32_t ta
 /* Kernel shape.  RT_KERNEL_PERSISTENT: a resident grid of waves pulls work
  * items from a global counter and streams paths continuously (two items in
  * flight per wave) — brute force (RT_ACCEL_NONE) only: with the grid or the
- * BVH the grid kernel runs, which measured faster (DESIGN.md §4.6).
+ * BVH the grid kernel runs, which measured faster (DESIGN.md §4.5).
  * RT_KERNEL_GRID: one wave per work item.  RT_KERNEL_AUTO (default):
  * persistent for brute-force strips (fewer than 6e6 tile-samples), grid
  * otherwise.  RT_KERNEL_QUEUE: CU-resident 16-wave blocks that share an LDS
  * pool of rays binned by the length of their next grid walk (grid scenes,
- * tiles of 8 or 16 columns; otherwise as RT_KERNEL_AUTO; DESIGN.md §4.7).
+ * tiles of 8 or 16 columns; otherwise as RT_KERNEL_AUTO; DESIGN.md §4.6).
  * All give bit-identical images. */
 enum { RT_KERNEL_GRID = 0, RT_KERNEL_PERSISTENT = 1, RT_KERNEL_AUTO = 2, RT_KERNEL_QUEUE = 3 };
 int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind);
@@ -149,16 +149,16 @@ int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind);
  * reference's hittable_list::hit (hittable_list.h:20-34).  RT_ACCEL_BVH: the
  * spheres much larger than the median (the ground) brute force, the rest
  * through a BVH with conservative boxes and an order-independent tie rule:
- * the same closest hit, bit for bit (DESIGN.md §4.4).  rt_ctx_accel_info
+ * the same closest hit, bit for bit (DESIGN.md §4.3).  rt_ctx_accel_info
  * reports the split (big spheres, BVH nodes) of the current scene.
  * RT_ACCEL_GRID: the same split, the small spheres in a uniform grid walked
- * by a 3D DDA (DESIGN.md §4.5); same closest hit bit for bit.
+ * by a 3D DDA (DESIGN.md §4.4); same closest hit bit for bit.
  * rt_ctx_grid_info reports its cells per axis, references and LDS bytes
  * (RT_EUNSUPPORTED when the scene has no grid: the render then uses brute
  * force). */
 enum { RT_ACCEL_NONE = 0, RT_ACCEL_BVH = 1, RT_ACCEL_GRID = 2 };
 /* (a new context starts with RT_ACCEL_GRID: same image as brute force, and
- * the fastest on the reference's scenes — DESIGN.md §4.5) */
+ * the fastest on the reference's scenes — DESIGN.md §4.4) */
 
 /* Dispatch order.  RT_ORDER_COST (default): every render counts world.hit
  * calls per tile and dispatches its tiles most-expensive-first (a GPU radix

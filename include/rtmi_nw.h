@@ -17,7 +17,7 @@
  * Conventions are those of rtmi.h: RT_OK / negative RT_E* returns (builders
  * return the new handle, >= 0, or a negative RT_E*), rt_last_error(), no
  * CPU fallback, per-pixel colour SUMS with row 0 at the bottom.  Differences
- * from the reference's semantics are listed in DESIGN.md §9.2.
+ * from the reference's semantics are listed in DESIGN.md §9.
  */
 #ifndef RTMI_NW_H
 #define RTMI_NW_H
@@ -83,7 +83,7 @@ int rt_nw_constant_medium(rt_nw_scene *s, int32_t boundary, double density, int3
  * Media are resolved before the other objects of a segment, and a medium's
  * hit hides its own boundary object when that is in the world too (the
  * reference visits constant_medium after its boundary, main.cu:386-391, and
- * constant_medium::hit ignores t_max).  DESIGN.md §9.2. */
+ * constant_medium::hit ignores t_max).  DESIGN.md §9. */
 int rt_nw_medium_samples(rt_nw_scene *s, int32_t medium, int32_t samples);
 /* hittable_list / bvh_node of objects (one handle for the set). */
 int rt_nw_group(rt_nw_scene *s, const int32_t *objects, int32_t n);
@@ -112,7 +112,7 @@ int rt_nw_xorwow_uniforms(uint64_t seed, int32_t n, float *out);
 /* Flattened view of a scene (what the device renders), for tests and the
  * oracle.  Pointers stay valid until the scene is modified or destroyed.
  *   obj  : n_obj * 16 floats: g0[4] g1[4] g2[4] then kind, mat, inst, aux as
- *          int32 bit patterns (layout: DESIGN.md §9.1; aux: medium -> boundary
+ *          int32 bit patterns (layout: DESIGN.md §9; aux: medium -> boundary
  *          kind | samples << 8, other -> insertion index of the medium whose
  *          boundary it is + 1, or 0)
  *   inst : n_inst * 8 floats: cos, sin, off.x, off.y, off.z, flags(int bits), 0, 0
@@ -130,7 +130,7 @@ typedef struct rt_nw_flat {
 } rt_nw_flat;
 int rt_nw_scene_flat(rt_nw_scene *s, rt_nw_flat *out);
 /* Host only (no device needed): the uniform grid rt_nw_ctx_set_scene would
- * build for this scene (DESIGN.md §9.5) — cells per axis (zeros: no grid),
+ * build for this scene (DESIGN.md §9) — cells per axis (zeros: no grid),
  * the fullest cell's object count, the brute-force list's length and the
  * total cell references.  Any output may be null. */
 int rt_nw_scene_grid_stats(rt_nw_scene *s, int32_t *dims3, int32_t *max_cell, int32_t *n_big, int32_t *n_refs);
@@ -143,9 +143,9 @@ int rt_nw_ctx_set_scene(rt_nw_ctx *ctx, rt_nw_scene *s);
 /* n_prims, n_nodes of the resident BVH */
 int rt_nw_ctx_info(rt_nw_ctx *ctx, int32_t *n_prims, int32_t *n_nodes);
 /* Closest-hit structure over the non-media objects (media are always tested
- * first, DESIGN.md §9.2).  RT_NW_ACCEL_BVH: the SAH BVH (skip-link walk).
+ * first, DESIGN.md §9).  RT_NW_ACCEL_BVH: the SAH BVH (skip-link walk).
  * RT_NW_ACCEL_GRID: a uniform grid walked by a 3D DDA, objects much larger
- * than the median in a brute-force list beside it (DESIGN.md §9.5); offered
+ * than the median in a brute-force list beside it (DESIGN.md §9); offered
  * when the scene has one (rt_nw_ctx_accel_info).  RT_NW_ACCEL_AUTO (a new
  * context's setting): the grid when it is balanced (at most 24 objects in
  * any cell), else the BVH.  All give the same closest hit, so the same image

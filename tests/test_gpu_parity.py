@@ -363,7 +363,7 @@ def test_bvh_bit_exact_vs_oracle_final(kernel, accel, final_world, final_rendere
     assert nb == 4 and nn > 100  # ground + the three r=1 spheres stay brute force
     dims, nrefs, lds = final_renderer.grid_info()
     # the record slots + 1.5 KB of shared accumulators + ~0.2 KB of static LDS
-    # must stay within 20 KB per 4-wave block: 8 blocks per CU (DESIGN §4.5)
+    # must stay within 20 KB per 4-wave block: 8 blocks per CU (DESIGN §4.4)
     assert dims[1] == 1 and dims[0] * dims[2] >= 400 and nrefs >= 483 and lds + 1536 + 256 <= 20480, (dims, nrefs, lds)
     final_renderer.set_accel(accel)
     final_renderer.set_kernel(kernel)
@@ -491,7 +491,7 @@ def test_bvh_adversarial_rays_equal_brute_force(accel, final_world):
 
 
 def test_grid_general_and_one_layer_walks(final_world):
-    """The grid kernel has two walks (DESIGN.md §4.5): the one-layer walk for
+    """The grid kernel has two walks (DESIGN.md §4.4): the one-layer walk for
     grids with a single cell layer in y (the final scene: asserted) and the
     general 3D walk (a scene of spheres filling a cube: asserted ny > 1).
     For the 3D scene, 200 k adversarial rays through rt_ctx_debug_hits (the

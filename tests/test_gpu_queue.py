@@ -1,4 +1,4 @@
-"""The queue kernel (RT_KERNEL_QUEUE, DESIGN.md §4.7) against the oracle and
+"""The queue kernel (RT_KERNEL_QUEUE, DESIGN.md §4.6) against the oracle and
 the other kernels, bit for bit.
 
 Rays migrate between the waves of a block through the LDS pool and end in

@@ -15,7 +15,7 @@ def test_job_division_by_reciprocal_multiply_is_exact():
 
 
 def test_camera_ray_pool_assigns_the_same_jobs():
-    """render_kernel's camera-ray pool (DESIGN.md §4.6), restated on the host:
+    """render_kernel's camera-ray pool (DESIGN.md §4.5), restated on the host:
     lane L of the pool holds job pbase + L; in a pass where the lanes in mask m
     finished, the lane of rank r among them takes slot ppos + r, refilling the
     pool (pbase += 64) when it runs out.  Every lane gets exactly the job the

@@ -1,5 +1,5 @@
 """The built library's render kernels keep the register budget DESIGN.md
-§4.3/§8 rests on (no GPU needed): the one-layer grid kernel that renders the
+§4.5/§8 rests on (no GPU needed): the one-layer grid kernel that renders the
 final scene, render_kernel<8, true, 3>, and its cost probe <8, false, 3> use
 at most 64 VGPRs (8 waves per SIMD) and no private segment (no spills), and
 their static LDS leaves the grid's record slots room for 8 blocks per CU.

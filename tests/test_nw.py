@@ -194,7 +194,7 @@ def test_cli_usage_without_gpu():
 
 
 def test_grid_stats_of_presets():
-    """The uniform grid the device would build (host only, DESIGN.md §9.5):
+    """The uniform grid the device would build (host only, DESIGN.md §9):
     the motion-blur random_scene gets a balanced grid with the R = 1000
     ground in the brute-force list; the final scene's 1000-sphere cluster
     fills a few cells (auto renders it with the BVH)."""

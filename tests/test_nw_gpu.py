@@ -32,7 +32,7 @@ def earth():
 @pytest.mark.parametrize("which", list(range(1, 9)))
 def test_presets_bit_exact_vs_oracle(which, accel, earth):
     """Both closest-hit structures (the BVH and the uniform grid with its
-    brute-force list, DESIGN.md §9.5) against the oracle's plain list."""
+    brute-force list, DESIGN.md §9) against the oracle's plain list."""
     W, H, spp = 29, 23, 3  # ragged: partial 8x8 tiles on both axes
     s, cam = nw.preset(which, image=earth, aspect=W / H)
     r = nw.NwRenderer(s)
@@ -98,7 +98,7 @@ def _quantize(sums, spp):
 def test_final_scene_statistics_vs_reference_gallery(earth):
     """The final scene at 800x800 (main.cu:520-523) vs the reference's own
     render at 5000 spp, by 50x50-pixel tile means (printed for the record).
-    What remains is our 1024-spp noise and the deviations of DESIGN.md §9.2
+    What remains is our 1024-spp noise and the deviations of DESIGN.md §9
     (our sample stream vs per-pixel curand, the JPEG decoder)."""
     W = H = 800
     spp = 1024
@@ -119,7 +119,7 @@ def test_final_scene_statistics_vs_reference_gallery(earth):
           f"vs gallery: bias {d.mean():.3f} MAE {np.abs(d).mean():.3f} tile MAE {td.mean():.3f} tile max {td.max():.2f} "
           f"tile p95 {np.percentile(td, 95):.2f}")
     # measured at 1024 spp: bias -0.55, tile MAE 0.59 (before the medium rules of
-    # DESIGN.md §9.2: bias -12.7, tile MAE 12.9)
+    # DESIGN.md §9: bias -12.7, tile MAE 12.9)
     assert abs(d.mean()) < 1.0 and td.mean() < 1.0 and td.max() < 6
 
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# The queue kernel (DESIGN.md §4.7): its parity tests (tests/test_gpu_queue.py),
+# The queue kernel (DESIGN.md §4.6): its parity tests (tests/test_gpu_queue.py),
 # then config 2 and the 1/8 strip through the grid kernel and the queue
 # kernel, interleaved twice; QLIBS="<v> ..." adds library variants
 # (lib/librtmi_<v>.so, e.g. other bin / pool sizes) run with --kernel queue.

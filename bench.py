@@ -11,6 +11,12 @@ j % N), each rank renders its strip on its own GPU, and the strips are
 gathered to rank 0 with ONE RCCL gather (torch.distributed "nccl" = RCCL)
 inside the timed region.  Total work is fixed as N grows: scaling "strong".
 value = W*H*spp*K / max-over-ranks(wall time of K steps) / 1e6.
+Steps alternate over two render contexts, each on a HIP stream with a
+hardware queue of its own (--pipeline 2, the default): step k+1's render is
+independent of step k's, so its first blocks fill the CUs that step k's last
+blocks leave idle (the end-of-dispatch drain).  Every step still
+renders the whole workload; --pipeline 1 runs them one after another on one
+context.
 `--gpus N` without a launcher environment starts the N ranks itself (a
 torch.distributed.run child of a parent that never touches the GPU) and
 refuses to run when fewer than N GPUs are visible.  After the timed region
@@ -226,6 +232,52 @@ class StubRenderer:
         if name.startswith("set_") or name == "close":
             return lambda *a, **k: None
         raise AttributeError(name)
+
+
+def hw_queue_streams(torch, dev, n):
+    """n HIP streams, each on a hardware queue of its own: created with
+    hipExtStreamCreateWithCUMask and every CU enabled (the runtime gives a
+    CU-masked stream its own queue; plain streams created after torch's stream
+    pool share queues, and two streams on one queue run their kernels one after
+    another, measured in profiles/r05/pipeline/).  Returns (torch streams,
+    destroy function)."""
+    import ctypes as C
+
+    hip = C.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    words = [0] * ((ncu + 31) // 32)
+    for c in range(ncu):
+        words[c // 32] |= 1 << (c % 32)
+    mask = (C.c_uint32 * len(words))(*words)
+    raw = []
+    for _ in range(n):
+        h = C.c_void_p()
+        rc = hip.hipExtStreamCreateWithCUMask(C.byref(h), C.c_uint32(len(words)), mask)
+        if rc != 0:
+            raise RuntimeError(f"bench: hipExtStreamCreateWithCUMask failed ({rc})")
+        raw.append(h.value)
+
+    def destroy():
+        torch.cuda.synchronize(dev)
+        for x in raw:
+            hip.hipStreamDestroy(C.c_void_p(x))
+
+    return [torch.cuda.ExternalStream(x, device=dev) for x in raw], destroy
+
+
+def busy_ms_per_launch(events):
+    """Mean GPU time per launch over (start, end) event pairs that may
+    overlap (launches on two streams): the union of their intervals / count."""
+    base = events[0][0]
+    iv = sorted((base.elapsed_time(a), base.elapsed_time(b)) for a, b in events)
+    total, cur_s, cur_e = 0.0, iv[0][0], iv[0][1]
+    for a, b in iv[1:]:
+        if a > cur_e:
+            total += cur_e - cur_s
+            cur_s, cur_e = a, b
+        else:
+            cur_e = max(cur_e, b)
+    return (total + cur_e - cur_s) / len(events)
 
 
 class StubEvent:
@@ -510,6 +562,9 @@ def main():
                     help="analysis only: render create_world case 1..8 at the nw_* workload's size instead")
     ap.add_argument("--nw-accel", choices=["auto", "bvh", "grid"], default="auto",
                     help="closest-hit structure of the nw_* workloads (rt_nw_ctx_set_accel; same image)")
+    ap.add_argument("--pipeline", type=int, choices=[1, 2], default=2,
+                    help="render contexts the steps alternate over, each on its own hardware queue (2: consecutive "
+                         "steps' renders may overlap; 1: one context, one stream)")
     ap.add_argument("--strip-of", type=int, default=0,
                     help="analysis only: time ONE rank's interleaved strip of an N-GPU run on this GPU")
     args = ap.parse_args()
@@ -535,49 +590,61 @@ def main():
 
     world = rt.random_scene()
     cam = rt.final_camera(W / H)
-    r = StubRenderer() if STUB else rt.Renderer(world, local_rank, tile_w=args.tile_w, chunk=args.chunk)
-    r.set_schedule(args.chunk, args.tail_spp, args.tail_chunk)
-    r.set_kernel(args.kernel)
-    r.set_accel(args.accel)
-    r.set_ordering(args.ordering)
+    npipe = 1 if STUB else args.pipeline
+
+    def make_renderer():
+        x = StubRenderer() if STUB else rt.Renderer(world, local_rank, tile_w=args.tile_w, chunk=args.chunk)
+        x.set_schedule(args.chunk, args.tail_spp, args.tail_chunk)
+        x.set_kernel(args.kernel)
+        x.set_accel(args.accel)
+        x.set_ordering(args.ordering)
+        return x
+
+    rs = [make_renderer() for _ in range(npipe)]  # the steps' render contexts (step k: rs[k % npipe])
+    r = rs[0]  # the context of the side launches below
     row0, row_step, nrows = rdist.strip_rows(H, rank, N)  # interleaved rows, row j -> rank j % N
     if args.strip_of > 1 and N == 1:  # analysis mode: one rank's share of an N-GPU render
         row0, row_step, nrows = rdist.strip_rows(H, 0, args.strip_of)
     nrows_valid = len(range(row0, H, row_step))  # rows of this strip inside the image
     strip = torch.empty((nrows, W, 3), dtype=torch.float32, device=dev)
-    # N > 1: two strip buffers, so that step k+1 renders into one while step
-    # k's gather still reads the other (the collective overlaps the next
-    # render; a buffer is rendered into again only after its gather is done)
-    strips = [strip] + ([torch.empty_like(strip)] if N > 1 else [])
+    # two strip buffers (N > 1 or two contexts): step k+1 renders into one
+    # while step k's render or gather still uses the other (a buffer is
+    # rendered into again only after its gather is done); buffer b is always
+    # rendered by context b % npipe on its stream
+    strips = [strip] + ([torch.empty_like(strip)] if N > 1 or npipe > 1 else [])
     tw = args.tile_w or rt.auto_tile_w(W, -(-(H - row0) // row_step) if row0 < H else 0)  # reported tile shape
     gathered = None
+    destroy_streams = None
     if STUB:
-        stream, Event = None, StubEvent
+        streams, Event = [None], StubEvent
 
         def sync():
             pass
 
-        def render_into(rows, buf):
-            r.render_rows(cam, W, H, SPP, DEPTH, SEED, *rows, buf)
+        def render_into(rows, buf, c=0):
+            rs[c].render_rows(cam, W, H, SPP, DEPTH, SEED, *rows, buf)
     else:
-        # a non-default stream: the kernel, its HIP events and the RCCL gather
-        # are all ordered on it (the null stream would bypass the events)
-        stream, Event = torch.cuda.Stream(dev), torch.cuda.Event
-        torch.cuda.set_stream(stream)
+        # non-default streams, one per context: each context's kernels, the
+        # HIP events around them and the RCCL gather of its strip are ordered
+        # on its stream (the null stream would bypass the events)
+        streams, destroy_streams = hw_queue_streams(torch, dev, npipe)
+        Event = torch.cuda.Event
+        torch.cuda.set_stream(streams[0])
 
         def sync():
             torch.cuda.synchronize(dev)
 
-        def render_into(rows, buf):
-            r.render_rows(cam, W, H, SPP, DEPTH, SEED, *rows, buf.data_ptr(), stream.cuda_stream)
+        def render_into(rows, buf, c=0):
+            rs[c].render_rows(cam, W, H, SPP, DEPTH, SEED, *rows, buf.data_ptr(), streams[c].cuda_stream)
 
+    stream = streams[0]  # the side launches' stream (context 0)
     ev, gev = [], []
 
-    def timed_render(rows=(row0, row_step, nrows), buf=strip):
+    def timed_render(rows=(row0, row_step, nrows), buf=strip, c=0):
         e0, e1 = Event(enable_timing=True), Event(enable_timing=True)
-        e0.record(stream)
-        render_into(rows, buf)
-        e1.record(stream)
+        e0.record(streams[c])
+        render_into(rows, buf, c)
+        e1.record(streams[c])
         return e0, e1
 
     pend = {}  # buffer -> (step, gathered strips, Work, source) of the gather in flight from it
@@ -591,14 +658,17 @@ def main():
 
     def step(record):
         b = nstep[0] % len(strips)
+        c = b % npipe  # this step's context and stream
         nstep[0] += 1
+        if not STUB:
+            torch.cuda.set_stream(streams[c])  # the gather below (and the wait on its buffer) on this stream
         if b in pend:  # this buffer's previous gather must be done before the render overwrites it
             collect(b)
         buf = strips[b]
         if record:
-            ev.append(timed_render(buf=buf))
+            ev.append(timed_render(buf=buf, c=c))
         else:
-            render_into((row0, row_step, nrows), buf)
+            render_into((row0, row_step, nrows), buf, c)
         if STALL_RANK == rank:  # test only: this rank stalls before its gather
             time.sleep(STALL_S)
         if N > 1:  # the single exchange step: strips -> rank 0 over RCCL/xGMI, overlapping the next render
@@ -614,7 +684,13 @@ def main():
     for _ in range(args.warmup):
         step(False)
     drain()
+    for c in range(min(args.warmup, npipe), npipe):
+        # a context the warmup steps did not reach renders its rows once,
+        # untimed, so that every timed step reuses its own context's cost map
+        render_into((row0, row_step, nrows), strips[c], c)
     sync()
+    if not STUB:
+        torch.cuda.set_stream(streams[0])
     if N > 1:
         collective("barrier before the timed region", dist.barrier)
     sync()
@@ -627,12 +703,18 @@ def main():
         collective("barrier after the timed region", dist.barrier)
     sync()
     elapsed = my_elapsed = time.perf_counter() - t0
+    if not STUB:
+        torch.cuda.set_stream(streams[0])
     if N > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
         collective("all_reduce(max) of the timed region", dist.all_reduce, t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    # GPU time per launch: the union of the launches' intervals / K (launches on
+    # two streams overlap at their ends); launch_ms = the mean of each launch's
+    # own start-to-end time, which counts the overlap once per launch
+    kernel_ms = busy_ms_per_launch(ev)
+    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     segs = r.last_segments()  # this rank's strip, last render
     dist_info = None
     if N > 1:
@@ -758,6 +840,10 @@ def main():
                      "none": "executed: segments x spheres x 18 FLOP (brute force)"}[args.accel],
             "flop_per_launch": flop_exec,
             "kernel_ms": round(kernel_ms, 3),
+            "kernel_ms_note": ("GPU time per launch: union of the timed launches' HIP-event intervals / steps (launches "
+                               "of consecutive steps overlap at their ends on two streams; launch_ms_mean counts the "
+                               "overlap in both)") if npipe > 1 else "mean HIP-event duration of the timed launches",
+            "launch_ms_mean": round(launch_ms, 3),
             "kernel_ms_max_rank": round(kernel_ms_max, 3),
             "segments_per_launch": segs,
             "segments_per_sample": round(total_segs / samples, 4),
@@ -830,6 +916,7 @@ def main():
                 "kernel": args.kernel,
                 "accel": args.accel,
                 "ordering": args.ordering,
+                "pipeline": npipe,
                 "timed_steps": ("each step re-renders the same workload; with ordering 'cost' it dispatches tiles by the "
                                 "previous identical render's per-tile cost map (RT_ORDER_COST): the first render of a "
                                 "layout (warmup) pays a 1-2 spp probe pass instead, see one_shot_msamples_per_s"
@@ -849,12 +936,19 @@ def main():
             line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)
         if gather_check is not None and not gather_check["bit_exact_vs_1gpu_frame"]:
-            r.close()
+            close_all(rs, destroy_streams)
             dist.destroy_process_group()
             sys.exit(3)
-    r.close()
+    close_all(rs, destroy_streams)
     if N > 1:
         dist.destroy_process_group()
+
+
+def close_all(rs, destroy_streams):
+    for x in rs:
+        x.close()
+    if destroy_streams:
+        destroy_streams()
 
 
 NW_PUBLISHED_MSPS = 1200 * 800 * 500 / 37.8792 / 1e6  # rt_next_week/cuda/README.md:167-174 (RTX 2060 Max-Q)
@@ -958,7 +1052,11 @@ def bench_nw(args):
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
         collective("all_reduce(max) of the timed region", dist.all_reduce, t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    # GPU time per launch: the union of the launches' intervals / K (launches on
+    # two streams overlap at their ends); launch_ms = the mean of each launch's
+    # own start-to-end time, which counts the overlap once per launch
+    kernel_ms = busy_ms_per_launch(ev)
+    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     segs = r.last_segments()
     flop_seg = nw_flop_per_segment(scene.flat())
     flop_rank = segs * flop_seg  # this rank's launch, brute-force equivalent

@@ -89,3 +89,20 @@ def test_executed_flop_counts_nodes_leaves_and_big_spheres():
     c = {"segments": 10, "node_visits": 100, "leaf_sphere_tests": 30, "big_spheres": 4}
     assert bench.executed_flop(c) == 100 * 25 + (30 + 40) * 18
     assert bench.executed_flop(c, "grid") == 10 * 25 + 100 * 5 + (30 + 40) * 18
+
+
+def test_busy_ms_per_launch_unions_overlapping_launches():
+    """roofline.kernel_ms under --pipeline 2: launches on two streams overlap;
+    the per-launch GPU time is the union of their intervals / count."""
+
+    class Ev:
+        def __init__(self, t):
+            self.t = t
+
+        def elapsed_time(self, other):
+            return other.t - self.t
+
+    pairs = lambda iv: [(Ev(a), Ev(b)) for a, b in iv]  # noqa: E731
+    assert bench.busy_ms_per_launch(pairs([(0, 10), (10, 20), (20, 30)])) == 10
+    assert bench.busy_ms_per_launch(pairs([(0, 20), (1, 21), (20, 40), (21, 41)])) == 41 / 4
+    assert bench.busy_ms_per_launch(pairs([(5, 6), (0, 2)])) == 1.5  # a gap is not counted; any order

@@ -27,3 +27,4 @@ echo "== rocprof kernel trace"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-exec-counts --timed-only > $OUT/kt_bench.json 2> $OUT/kt.err || exit 1
 cat $OUT/kt_bench.json
 find $OUT/kt -name "*kernel_stats.csv" -exec head -6 {} \;
+python3 tools/trace_busy.py $(find $OUT/kt -name "*kernel_trace.csv" | head -1) | tee $OUT/kt_busy.txt

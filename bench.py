@@ -254,7 +254,7 @@ def hw_queue_streams(torch, dev, n):
         h = C.c_void_p()
         rc = hip.hipExtStreamCreateWithCUMask(C.byref(h), C.c_uint32(len(words)), mask)
         if rc != 0:
-            raise RuntimeError(f"bench: hipExtStreamCreateWithCUMask failed ({rc})")
+            break
         raw.append(h.value)
 
     def destroy():
@@ -262,6 +262,10 @@ def hw_queue_streams(torch, dev, n):
         for x in raw:
             hip.hipStreamDestroy(C.c_void_p(x))
 
+    if len(raw) < n:  # the same steps on plain streams (correct; they may share a queue and not overlap)
+        print(f"bench: hipExtStreamCreateWithCUMask failed ({rc}): plain streams instead", file=sys.stderr, flush=True)
+        destroy()
+        return [torch.cuda.Stream(dev) for _ in range(n)], None
     return [torch.cuda.ExternalStream(x, device=dev) for x in raw], destroy
 
 

@@ -12,4 +12,5 @@ for w in ${WORKLOADS:-config4 config5}; do
   python -c "import json; d=json.load(open('$OUT/$w.json')); r=d['roofline']; print('$w', d['value'], d['ms_per_step'], r['kernel_ms'], r['frac'], r['work_equivalent_frac'])"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$w -o kt -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-exec-counts --timed-only --workload $w > $OUT/kt_$w.json 2> $OUT/kt_$w.err || { tail -5 $OUT/kt_$w.err; exit 1; }
   find $OUT/kt_$w -name "*kernel_stats.csv" -exec head -3 {} \; | cut -c1-160
+  python3 tools/trace_busy.py $(find $OUT/kt_$w -name "*kernel_trace.csv" | head -1) | tee $OUT/kt_${w}_busy.txt
 done

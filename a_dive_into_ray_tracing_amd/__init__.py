@@ -186,6 +186,11 @@ class Renderer:
     def set_schedule(self, chunk=0, tail_spp=-1, tail_chunk=0):
         check(self.L.rt_ctx_set_schedule(self._h, chunk, tail_spp, tail_chunk), "rt_ctx_set_schedule")
 
+    def set_overlap(self, overlapped=True):
+        """Launch-mode hint: this context's renders overlap another context's on
+        the same device (rt_ctx_set_overlap); fewer, longer work items."""
+        check(self.L.rt_ctx_set_overlap(self._h, int(bool(overlapped))), "rt_ctx_set_overlap")
+
     KERNELS = {"grid": 0, "persistent": 1, "auto": 2, "queue": 3}  # RT_KERNEL_* (include/rtmi.h)
 
     def set_kernel(self, kind="auto"):

@@ -74,6 +74,7 @@ SIGNATURES = {
     "rt_ctx_set_scene": (C.c_int, [C.c_void_p, C.POINTER(RtScene)]),
     "rt_ctx_set_tuning": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "rt_ctx_set_schedule": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
+    "rt_ctx_set_overlap": (C.c_int, [C.c_void_p, C.c_int32]),
     "rt_ctx_set_kernel": (C.c_int, [C.c_void_p, C.c_int32]),
     "rt_ctx_set_accel": (C.c_int, [C.c_void_p, C.c_int32]),
     "rt_ctx_set_ordering": (C.c_int, [C.c_void_p, C.c_int32]),

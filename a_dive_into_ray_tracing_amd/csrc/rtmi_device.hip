@@ -1504,9 +1504,14 @@ struct rt_ctx {
   int32_t probe_spp = std::getenv("RTMI_PROBE_SPP") ? std::atoi(std::getenv("RTMI_PROBE_SPP")) : 0;
   bool probing = false;
   // automatic item size of the grid kernel: ~want_items items of item_min..125
-  // samples (RTMI_WANT_ITEMS / RTMI_ITEM_MIN override, for A/B)
-  int64_t want_items = std::getenv("RTMI_WANT_ITEMS") ? std::atoll(std::getenv("RTMI_WANT_ITEMS")) : 60000;
-  int32_t item_min = std::getenv("RTMI_ITEM_MIN") ? std::atoi(std::getenv("RTMI_ITEM_MIN")) : 24;
+  // samples; 0 = the default of the launch mode below (RTMI_WANT_ITEMS /
+  // RTMI_ITEM_MIN override, for A/B)
+  int64_t want_items = std::getenv("RTMI_WANT_ITEMS") ? std::atoll(std::getenv("RTMI_WANT_ITEMS")) : 0;
+  int32_t item_min = std::getenv("RTMI_ITEM_MIN") ? std::atoi(std::getenv("RTMI_ITEM_MIN")) : 0;
+  // rt_ctx_set_overlap: this context's launches run beside another context's
+  // on the same device, so a launch's dispatch tail is filled by the other's
+  // blocks and fewer, longer items pay less per-item overhead
+  bool overlap = false;
 };
 
 namespace rtmi {
@@ -1986,6 +1991,13 @@ RTMI_EXPORT int rt_ctx_set_schedule(rt_ctx *ctx, int32_t chunk, int32_t tail_spp
   return RT_OK;
 }
 
+RTMI_EXPORT int rt_ctx_set_overlap(rt_ctx *ctx, int32_t overlapped) {
+  if (!ctx) return set_error(RT_EINVAL, "null ctx");
+  if (overlapped != 0 && overlapped != 1) return set_error(RT_EINVAL, "overlapped must be 0 or 1");
+  ctx->overlap = overlapped != 0;
+  return RT_OK;
+}
+
 RTMI_EXPORT int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind) {
   if (!ctx) return set_error(RT_EINVAL, "null ctx");
   if (kind != RT_KERNEL_GRID && kind != RT_KERNEL_PERSISTENT && kind != RT_KERNEL_AUTO && kind != RT_KERNEL_QUEUE)
@@ -2183,8 +2195,13 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     // rank's 1/8 strip 8.06 ms with 7, 7.37 with 14, 7.18 with 21, 7.27 with
     // 32 (profiles/r01/session6/chunk_ab.txt): long items pay the per-item
     // ramp-down less often, short ones shorten a small grid's dispatch tail
-    const int64_t want_items = ctx->want_items;
-    chunk1 = int32_t(std::min<int64_t>(125, std::max<int64_t>(ctx->item_min, tile_samples / want_items)));
+    // With overlapping launches (rt_ctx_set_overlap) ~15 k items of >= 63
+    // samples: one rank's strip of config 2 at 1/2, 1/4, 1/8 of the rows
+    // 9.54 / 4.89-4.92 / 2.53 ms against 9.87 / 5.14 / 2.64 with the
+    // single-launch default (profiles/r05/pipeline/ab_items.txt)
+    const int64_t want_items = ctx->want_items > 0 ? ctx->want_items : (ctx->overlap ? 15000 : 60000);
+    const int64_t item_min = ctx->item_min > 0 ? ctx->item_min : (ctx->overlap ? 63 : 24);
+    chunk1 = int32_t(std::min<int64_t>(125, std::max<int64_t>(item_min, tile_samples / want_items)));
   }
   if (chunk2 <= 0) chunk2 = std::max(1, chunk1 / 4);
   if (tail < 0 || queue) tail = 0;  // automatic: no short-item phase (it measured no better)

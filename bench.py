@@ -602,6 +602,8 @@ def main():
         x.set_kernel(args.kernel)
         x.set_accel(args.accel)
         x.set_ordering(args.ordering)
+        if npipe > 1:  # the launches of the two contexts overlap: fewer, longer items (rt_ctx_set_overlap)
+            x.set_overlap(True)
         return x
 
     rs = [make_renderer() for _ in range(npipe)]  # the steps' render contexts (step k: rs[k % npipe])

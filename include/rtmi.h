@@ -131,6 +131,14 @@ int rt_ctx_set_tuning(rt_ctx *ctx, int32_t tile_w, int32_t chunk);
  * `chunk` samples, the last tail_spp in items of `tail_chunk`, dispatched
  * last (0 / -1 = automatic).  Does not change the image. */
 int rt_ctx_set_schedule(rt_ctx *ctx, int32_t chunk, int32_t tail_spp, int32_t tail_chunk);
+/* Launch-mode hint (MI355X extension, no reference counterpart): overlapped =
+ * 1 when this context's renders run concurrently with another context's on
+ * the same device (e.g. consecutive frames alternating over two contexts on
+ * streams of their own hardware queues, bench.py --pipeline 2): the other
+ * launch fills this one's dispatch tail, so the automatic schedule uses fewer,
+ * longer work items.  0 (default) = launches run one at a time.  Does not
+ * change the image. */
+int rt_ctx_set_overlap(rt_ctx *ctx, int32_t overlapped);
 
 /* Kernel shape.  RT_KERNEL_PERSISTENT: a resident grid of waves pulls work
  * items from a global counter and streams paths continuously (two items in

@@ -829,6 +829,37 @@ def test_config3_strips_unpermute_to_config2_frame(G, config2, final_world):
     assert np.array_equal(rdist.unpermute(strips, H), img)
 
 
+def test_overlapped_contexts_strips_equal_frame(config2, final_world):
+    """bench.py --pipeline 2: two contexts with the overlap hint
+    (rt_ctx_set_overlap: fewer, longer work items) render the 8 strips of
+    config 2 on two streams, enqueued back to back so their launches run
+    concurrently; the un-permuted strips are the one-GPU frame bit for bit."""
+    torch = pytest.importorskip("torch")
+    from a_dive_into_ray_tracing_amd import dist as rdist
+
+    cam, img = config2
+    W, H, S, G = 1200, 800, 500, 8
+    rs = [rt.Renderer(final_world, 0) for _ in range(2)]
+    streams = [torch.cuda.Stream("cuda:0") for _ in range(2)]
+    strips, chunks = [], set()
+    try:
+        for x in rs:
+            x.set_overlap(True)
+        for g in range(G):
+            row0, step, nrows = rdist.strip_rows(H, g, G)
+            s = torch.full((nrows, W, 3), -1.0, dtype=torch.float32, device="cuda:0")
+            rs[g % 2].render_rows(cam, W, H, S, 50, SEED, row0, step, nrows, s.data_ptr(), streams[g % 2].cuda_stream)
+            chunks.add(rs[g % 2].last_schedule()["chunk"])
+            strips.append(s)
+        torch.cuda.synchronize()
+        assert rt.load().rt_ctx_set_overlap(rs[0]._h, 2) == -1  # RT_EINVAL: the hint is 0 or 1
+    finally:
+        for x in rs:
+            x.close()
+    assert chunks == {63}, chunks  # ~15 k items of >= 63 samples (the single-launch default: 21)
+    assert np.array_equal(rdist.unpermute([s.cpu().numpy() for s in strips], H), img)
+
+
 @pytest.mark.parametrize("which", [0, 1], ids=["sqrt", "reciprocal"])
 def test_exact_math_exhaustive(which):
     """The kernels' short correctly rounded sqrt and reciprocal (rtmi_path.h

@@ -594,7 +594,7 @@ def main():
 
     world = rt.random_scene()
     cam = rt.final_camera(W / H)
-    npipe = 1 if STUB else args.pipeline
+    npipe = args.pipeline  # (the stub rehearses the same alternation over two stand-in contexts)
 
     def make_renderer():
         x = StubRenderer() if STUB else rt.Renderer(world, local_rank, tile_w=args.tile_w, chunk=args.chunk)
@@ -622,7 +622,7 @@ def main():
     gathered = None
     destroy_streams = None
     if STUB:
-        streams, Event = [None], StubEvent
+        streams, Event = [None] * npipe, StubEvent
 
         def sync():
             pass

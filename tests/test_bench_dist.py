@@ -17,12 +17,15 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("n", [2, 3])
-def test_bench_n_ranks_line_schema(n, tmp_path):
+@pytest.mark.parametrize("n,pipeline", [(2, 2), (3, 2), (2, 1)])
+def test_bench_n_ranks_line_schema(n, pipeline, tmp_path):
+    """pipeline 2 (the default): the steps alternate over two render contexts
+    and two strip buffers; 3 timed steps reuse a buffer after its gather."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     env.update(RTMI_DIST_BACKEND="gloo", RTMI_BENCH_STUB="1", OMP_NUM_THREADS="1")
-    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--steps", "2", "--warmup", "1"],
-                       capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    steps = 3
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--steps", str(steps), "--warmup", "1",
+                        "--pipeline", str(pipeline)], capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
     assert p.returncode == 0, p.stderr[-3000:]
     lines = p.stdout.splitlines()
     # rank 0 prints ONE line and nothing else reaches stdout (gloo's start-up
@@ -30,7 +33,8 @@ def test_bench_n_ranks_line_schema(n, tmp_path):
     assert len(lines) == 1 and lines[0].startswith("{"), p.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["stub"] is True and d["data"].startswith("STUB")
-    assert d["n_gpus"] == n and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "strong"
+    assert d["n_gpus"] == n and d["steps"] == steps and d["warmup"] == 1 and d["scaling"] == "strong"
+    assert d["config"]["pipeline"] == pipeline
     assert d["unit"] == "Msamples/s" and d["value"] > 0 and d["ms_per_step"] > 0
     assert d["config"]["partition"] == "interleaved rows, one RCCL gather"
     di = d["dist"]

@@ -3,6 +3,8 @@
 # interleaved 1/N strip (bench.py --strip-of N) against the whole frame on one
 # GPU, N = 2, 4, 8, for config 2 and config 5.  A ceiling, not a scaling
 # measurement: no gather, no launch skew, one GPU.  Table in $OUT/strips.txt.
+# PIPELINE (default 1: one context, one launch at a time, as the round-5 table
+# in profiles/r05/strips/; 2: bench.py's default, steps overlapping).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -13,7 +15,7 @@ for w in config2 config5; do
   for n in 1 2 4 8; do
     so=""; [ $n -gt 1 ] && so="--strip-of $n"
     timeout -k 10 300 python -u bench.py --workload $w --steps $steps --warmup 1 --no-cpu-baseline --no-exec-counts \
-      --timed-only $so > $OUT/${w}_$n.json 2> $OUT/${w}_$n.err || { tail $OUT/${w}_$n.err; exit 1; }
+      --timed-only --pipeline ${PIPELINE:-1} $so > $OUT/${w}_$n.json 2> $OUT/${w}_$n.err || { tail $OUT/${w}_$n.err; exit 1; }
     echo "$w 1/$n $(python -c "import json; print(json.load(open('$OUT/${w}_$n.json'))['roofline']['kernel_ms'])")"
   done
 done

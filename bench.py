@@ -566,7 +566,7 @@ def main():
                     help="analysis only: render create_world case 1..8 at the nw_* workload's size instead")
     ap.add_argument("--nw-accel", choices=["auto", "bvh", "grid"], default="auto",
                     help="closest-hit structure of the nw_* workloads (rt_nw_ctx_set_accel; same image)")
-    ap.add_argument("--pipeline", type=int, choices=[1, 2], default=2,
+    ap.add_argument("--pipeline", type=int, choices=[1, 2, 3], default=2,
                     help="render contexts the steps alternate over, each on its own hardware queue (2: consecutive "
                          "steps' renders may overlap; 1: one context, one stream)")
     ap.add_argument("--strip-of", type=int, default=0,
@@ -617,7 +617,7 @@ def main():
     # while step k's render or gather still uses the other (a buffer is
     # rendered into again only after its gather is done); buffer b is always
     # rendered by context b % npipe on its stream
-    strips = [strip] + ([torch.empty_like(strip)] if N > 1 or npipe > 1 else [])
+    strips = [strip] + [torch.empty_like(strip) for _ in range(max(npipe, 2 if N > 1 else 1) - 1)]
     tw = args.tile_w or rt.auto_tile_w(W, -(-(H - row0) // row_step) if row0 < H else 0)  # reported tile shape
     gathered = None
     destroy_streams = None

@@ -243,7 +243,10 @@ def hw_queue_streams(torch, dev, n):
     destroy function)."""
     import ctypes as C
 
-    hip = C.CDLL("libamdhip64.so")
+    # the HIP runtime this process already uses (torch's), not a second copy
+    with open("/proc/self/maps") as f:
+        path = next((ln.split()[-1] for ln in f if "libamdhip64" in ln), "libamdhip64.so")
+    hip = C.CDLL(path)
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     words = [0] * ((ncu + 31) // 32)
     for c in range(ncu):

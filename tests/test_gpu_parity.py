@@ -128,6 +128,32 @@ def test_fast_kernel_bit_exact_vs_oracle_learn(W, H, S, depth, learn_renderer):
     assert np.array_equal(got, want), np.abs(got - want).max()
 
 
+@pytest.mark.parametrize("W,H,S", [(2, 2, 3), (2, 17, 5), (97, 2, 4), (2, 2, 33), (3, 65, 17), (2, 2, 70000)])
+def test_degenerate_shapes_bit_exact_vs_oracle(W, H, S, final_world):
+    """The smallest images the reference's camera allows (u, v divide by W - 1
+    and H - 1: at least 2 x 2; one pixel wide or tall is RT_EINVAL), tiles
+    mostly empty, and 2 x 2 pixels at 70 000 spp (more than the 65 535
+    samples an item may hold: two items each), through the default path
+    (uniform grid, cost-ordered, the probe for spp >= 16), against the
+    oracle; twice, so the second render runs on the first one's cost map."""
+    cam = rt.final_camera(W / H)
+    r = rt.Renderer(final_world, 0)
+    try:
+        for w, h in ((1, H), (W, 1)):
+            with pytest.raises(rt.RTError, match="RT_EINVAL"):
+                r.render(cam, w, h, S, 50, SEED)
+        first = r.render(cam, W, H, S, 50, SEED)
+        second = r.render(cam, W, H, S, 50, SEED)
+        segs = r.last_segments()
+        sch = r.last_schedule()
+    finally:
+        r.close()
+    assert sch["bvh"] == 2 and sch["chunk"] <= 65535, sch
+    want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
+    assert np.array_equal(first, want) and np.array_equal(second, want)
+    assert segs == O.fast_segments(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
+
+
 def test_max_depth_zero_is_black(learn_renderer):
     got = learn_renderer.render(rt.learn_camera(), 16, 9, 4, 0, SEED)
     assert not got.any()

@@ -154,6 +154,56 @@ def test_degenerate_shapes_bit_exact_vs_oracle(W, H, S, final_world):
     assert segs == O.fast_segments(o_scene(final_world), o_cam(cam), W, H, S, 50, SEED)
 
 
+@pytest.mark.parametrize("case", ["pinhole", "inside_glass", "vfov_1", "vfov_170", "seed_0", "seed_max", "depth_500",
+                                  "below_ground"])
+def test_camera_seed_depth_edge_cases_bit_exact_vs_oracle(case, final_world):
+    """Cameras and arguments away from the reference's defaults, through the
+    default path (grid, cost-ordered) against the oracle: a pinhole (aperture
+    0, rays from one point), the eye inside the big glass sphere (every
+    primary ray starts inside a dielectric), a 1° and a 170° field of view,
+    seeds 0 and 2^64 - 1, depth 500 (deep glass paths), and the eye inside
+    the ground sphere looking up (every ray leaves the R = 1000 sphere from
+    inside).  The world.hit count is compared too."""
+    W, H, S, depth, seed = 48, 32, 6, 50, SEED
+    lookfrom, lookat, vfov, aperture, focus = (13, 2, 3), (0, 0, 0), 20.0, 0.1, 10.0
+    if case == "pinhole":
+        aperture = 0.0
+    elif case == "inside_glass":
+        lookfrom, lookat, focus = (0, 1.2, 0.3), (4, 1, 0), 4.0
+    elif case == "vfov_1":
+        vfov = 1.0
+    elif case == "vfov_170":
+        vfov = 170.0
+    elif case == "seed_0":
+        seed = 0
+    elif case == "seed_max":
+        seed = 2**64 - 1
+    elif case == "depth_500":
+        depth = 500
+    elif case == "below_ground":
+        lookfrom, lookat, focus = (1, -3, 2), (0, 5, 0), 8.0
+    cam = rt.camera(lookfrom, lookat, (0, 1, 0), vfov, W / H, aperture, focus)
+    r = rt.Renderer(final_world, 0)
+    try:
+        got = r.render(cam, W, H, S, depth, seed)
+        segs = r.last_segments()
+    finally:
+        r.close()
+    want = O.fast_render(o_scene(final_world), o_cam(cam), W, H, S, depth, seed)
+    assert np.array_equal(got, want), np.abs(got - want).max()
+    assert segs == O.fast_segments(o_scene(final_world), o_cam(cam), W, H, S, depth, seed)
+
+
+def test_max_depth_limit(learn_renderer):
+    """max_depth lives in the low 24 bits of a path's register: 2^24 - 1 is
+    accepted, 2^24 refused (RT_EINVAL), as is a negative depth."""
+    cam = rt.learn_camera(2.0)
+    learn_renderer.render(cam, 4, 2, 1, (1 << 24) - 1, SEED)
+    for bad in (1 << 24, -1):
+        with pytest.raises(rt.RTError, match="RT_EINVAL"):
+            learn_renderer.render(cam, 4, 2, 1, bad, SEED)
+
+
 def test_max_depth_zero_is_black(learn_renderer):
     got = learn_renderer.render(rt.learn_camera(), 16, 9, 4, 0, SEED)
     assert not got.any()

@@ -194,6 +194,40 @@ def test_camera_seed_depth_edge_cases_bit_exact_vs_oracle(case, final_world):
     assert segs == O.fast_segments(o_scene(final_world), o_cam(cam), W, H, S, depth, seed)
 
 
+@pytest.mark.parametrize("n", [3000, 70000])
+def test_large_scenes_bit_exact_vs_oracle(n):
+    """Scenes far larger than the final scene's 487 spheres: each structure is
+    used only when it fits its LDS budget (the BVH also needs < 65 536
+    spheres), otherwise the render runs brute force; whichever path runs
+    (read back from the schedule), the image and world.hit count equal the
+    oracle's, for every accel setting."""
+    g = np.random.default_rng(n)
+    c = np.column_stack([g.uniform(-40, 40, n), g.uniform(0.05, 0.3, n), g.uniform(-40, 40, n)])
+    rad = g.uniform(0.03, 0.2, n)
+    kinds = g.integers(0, 3, n).astype(np.int32)
+    params = np.column_stack([g.uniform(0.1, 0.9, (n, 3)), np.where(kinds == 2, 1.5, g.uniform(0, 0.5, n))])
+    cr = np.vstack([[0, -1000, 0, 1000], np.column_stack([c, rad])])
+    kinds = np.concatenate([[0], kinds]).astype(np.int32)
+    params = np.vstack([[0.5, 0.5, 0.5, 0], params])
+    world = rt.World(cr, kinds, params)
+    W, H, S = 24, 16, 2
+    cam = rt.camera((20, 3, 12), (0, 0, 0), (0, 1, 0), 30.0, W / H, 0.05, 20.0)
+    want = O.fast_render(o_scene(world), o_cam(cam), W, H, S, 50, SEED)
+    want_segs = O.fast_segments(o_scene(world), o_cam(cam), W, H, S, 50, SEED)
+    r = rt.Renderer(world, 0)
+    ran = set()
+    try:
+        for accel in ("grid", "bvh", "none"):
+            r.set_accel(accel)
+            got = r.render(cam, W, H, S, 50, SEED)
+            ran.add((accel, r.last_schedule()["bvh"]))
+            assert np.array_equal(got, want), (accel, np.abs(got - want).max())
+            assert r.last_segments() == want_segs, accel
+    finally:
+        r.close()
+    assert ("none", 0) in ran, ran
+
+
 def test_max_depth_limit(learn_renderer):
     """max_depth lives in the low 24 bits of a path's register: 2^24 - 1 is
     accepted, 2^24 refused (RT_EINVAL), as is a negative depth."""

@@ -1459,6 +1459,9 @@ struct rt_ctx {
   int32_t nbig_pairs = 0, nbig = 0;
   BvhNode *nodes = nullptr;
   int32_t nnodes = 0;
+  bool bvh_global = false;  // the BVH is over the LDS budget: walked in global memory
+  // RTMI_BVH_GLOBAL=1 (tests): the global-memory walk for any BVH
+  bool force_bvh_global = std::getenv("RTMI_BVH_GLOBAL") && std::atoi(std::getenv("RTMI_BVH_GLOBAL")) != 0;
   float4 *bvh_sph = nullptr;
   int32_t *bvh_idx = nullptr;
   int32_t nbvh_sph = 0;
@@ -1947,10 +1950,12 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
     ctx->nbig = int32_t(big.size());
     ctx->nbig_pairs = nb_pad / 2;
     ctx->nbvh_sph = int32_t(b.sph.size());
-    // the BVH must fit in LDS beside the accumulators; otherwise it is not
-    // offered (RT_ACCEL_BVH renders brute force)
+    // the BVH is staged in LDS when it fits the budget beside the
+    // accumulators (and its 16-bit scene indices suffice); a larger one is
+    // walked in global memory (L2), still far fewer tests than brute force
     const size_t lds = bvh_lds_bytes(int32_t(b.nodes.size()), int32_t(b.sph.size()));
-    ctx->nnodes = lds <= kBvhLdsMax && n <= 65535 ? int32_t(b.nodes.size()) : 0;
+    ctx->nnodes = int32_t(b.nodes.size());
+    ctx->bvh_global = ctx->force_bvh_global || !(lds <= kBvhLdsMax && n <= 65535);
     // uniform grid over the same small spheres
     ctx->grid_ok = false;
     GridBuild gb;
@@ -2031,7 +2036,7 @@ RTMI_EXPORT int rt_ctx_set_tuning(rt_ctx *ctx, int32_t tile_w, int32_t chunk) {
 namespace {
 
 size_t accel_lds_bytes(const Accel &acc, int kind) {
-  if (kind == 1) return bvh_lds_bytes(acc.nnodes, acc.nsph);
+  if (kind == 1) return acc.bvh_global ? 0 : bvh_lds_bytes(acc.nnodes, acc.nsph);
   if (kind >= 2) return grid_lds_bytes(2 * acc.nbig_pairs, acc.grid.ncells, acc.grid.nrefs);
   return 0;
 }
@@ -2046,6 +2051,7 @@ Accel accel_of(const rt_ctx *ctx, int kind) {
     a.sph = ctx->bvh_sph;
     a.sph_idx = ctx->bvh_idx;
     a.nsph = ctx->nbvh_sph;
+    a.bvh_global = ctx->bvh_global;
   } else if (kind >= 2) {
     a.sph = ctx->grid_sph;
     a.nsph = ctx->ngrid_sph;
@@ -2168,9 +2174,10 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   // (3: the grid has one cell layer in y and the grid kernel walks it with
   // the y stepping dropped, hit_world_grid<.., true>: the same cells, 3% faster
   // on config 2)
-  const int acc_kind = ctx->accel == RT_ACCEL_BVH && ctx->nnodes > 0
-                           ? 1
-                           : (ctx->accel == RT_ACCEL_GRID && ctx->grid_ok ? (ctx->grid.n[1] == 1 ? 3 : 2) : 0);
+  // (a grid that does not fit, e.g. thousands of spheres, leaves the BVH)
+  const int acc_kind = ctx->accel == RT_ACCEL_GRID && ctx->grid_ok
+                           ? (ctx->grid.n[1] == 1 ? 3 : 2)
+                           : (ctx->accel != RT_ACCEL_NONE && ctx->nnodes > 0 ? 1 : 0);
   const bool bvh = acc_kind != 0;
   // the queue kernel: grid scenes, when selected
   const bool queue = acc_kind >= 2 && ctx->kernel == RT_KERNEL_QUEUE && TW <= 16;

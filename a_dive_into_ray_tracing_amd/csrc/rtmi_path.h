@@ -463,6 +463,7 @@ struct Accel {
   const int32_t *sph_idx;    // BVH: the leaf spheres' scene indices
   int32_t nsph;              // float4s of sph
   GridDesc grid;             // RT_ACCEL_GRID only
+  int32_t bvh_global;        // BVH too large for LDS: walked in global memory (L2)
 };
 
 // big_idx through the constant address space: wave-uniform scalar loads
@@ -482,11 +483,13 @@ __host__ __device__ constexpr size_t bvh_lds_bytes(int32_t nnodes, int32_t nsph)
 }
 
 __device__ __forceinline__ void stage_bvh(const Accel &g) {
-  const float4 *nodes = reinterpret_cast<const float4 *>(g.nodes);
-  for (int i = threadIdx.x; i < g.nnodes; i += blockDim.x) rtmi_bvh_lds[i] = nodes[i];
-  for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) rtmi_bvh_lds[g.nnodes + i] = g.sph[i];
-  uint16_t *idx = reinterpret_cast<uint16_t *>(rtmi_bvh_lds + g.nnodes + g.nsph);
-  for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) idx[i] = uint16_t(g.sph_idx[i]);
+  if (!g.bvh_global) {  // (a BVH over the LDS budget stays in global memory)
+    const float4 *nodes = reinterpret_cast<const float4 *>(g.nodes);
+    for (int i = threadIdx.x; i < g.nnodes; i += blockDim.x) rtmi_bvh_lds[i] = nodes[i];
+    for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) rtmi_bvh_lds[g.nnodes + i] = g.sph[i];
+    uint16_t *idx = reinterpret_cast<uint16_t *>(rtmi_bvh_lds + g.nnodes + g.nsph);
+    for (int i = threadIdx.x; i < g.nsph; i += blockDim.x) idx[i] = uint16_t(g.sph_idx[i]);
+  }
   __syncthreads();
 }
 
@@ -959,10 +962,9 @@ __device__ __forceinline__ int32_t hit_world_bvh(const Accel &acc_s, V3<float> o
               , bstats
 #endif
   );
-  // 2. the BVH (staged in LDS by stage_bvh), stackless: per-lane walk of the
-  // DFS node array with skip links
-  const float4 *lds_sph = rtmi_bvh_lds + acc_s.nnodes;
-  const uint16_t *lds_idx = reinterpret_cast<const uint16_t *>(rtmi_bvh_lds + acc_s.nnodes + acc_s.nsph);
+  // 2. the BVH (staged in LDS by stage_bvh, or in global memory when it is
+  // over the LDS budget: bvh_global, a wave-uniform choice), stackless:
+  // per-lane walk of the DFS node array with skip links
   // inverse direction with |d_i| clamped to >= 1e-20: no infinities, so no
   // 0*inf or inf-inf NaNs in the slab test (min/max would not ignore them
   // reliably).  The clamp moves the ray by a negligible angle; a ray running
@@ -972,51 +974,60 @@ __device__ __forceinline__ int32_t hit_world_bvh(const Accel &acc_s, V3<float> o
   // slab distances as one fma per plane: (b - o) * i = fma(b, i, -o*i); the
   // box margin covers the different rounding
   const float ox = -o.x * ix, oy = -o.y * iy, oz = -o.z * iz;
-  const uint4 *lds_node = reinterpret_cast<const uint4 *>(rtmi_bvh_lds);
   auto lo16 = [](uint32_t w) { return float(__builtin_bit_cast(_Float16, uint16_t(w))); };
   auto hi16 = [](uint32_t w) { return float(__builtin_bit_cast(_Float16, uint16_t(w >> 16))); };
-  int32_t node = 0;
-  while (node < acc_s.nnodes) {
-    const uint4 nd = lds_node[node];
-    const float tx0 = __builtin_fmaf(lo16(nd.x), ix, ox), tx1 = __builtin_fmaf(hi16(nd.x), ix, ox);
-    const float ty0 = __builtin_fmaf(lo16(nd.y), iy, oy), ty1 = __builtin_fmaf(hi16(nd.y), iy, oy);
-    const float tz0 = __builtin_fmaf(lo16(nd.z), iz, oz), tz1 = __builtin_fmaf(hi16(nd.z), iz, oz);
-    // slab interval clipped to [0, t_max].  No slack is needed: a sphere
-    // that can be hit lies >= the box margin inside the box, so its chord
-    // starts after tnear and ends before tfar by far more than rounding, and
-    // a hit at t_hit >= 0.001 with t_hit <= t_max (ties included) keeps the
-    // box entered.  Half-precision bounds only make the box larger.
-    const float tnear = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx0, tx1), __builtin_fminf(ty0, ty1)),
-                                        __builtin_fmaxf(__builtin_fminf(tz0, tz1), 0.0f));
-    const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx0, tx1), __builtin_fmaxf(ty0, ty1)),
-                                       __builtin_fminf(__builtin_fmaxf(tz0, tz1), t_max));
-    const bool enter = tnear <= tfar;
-    const int32_t link = int32_t(nd.w);
+  auto walk = [&](auto in_global) {
+    constexpr bool GLOBAL = decltype(in_global)::value;
+    const uint4 *nodes = GLOBAL ? reinterpret_cast<const uint4 *>(acc_s.nodes) : reinterpret_cast<const uint4 *>(rtmi_bvh_lds);
+    const float4 *sph = GLOBAL ? acc_s.sph : rtmi_bvh_lds + acc_s.nnodes;
+    const uint16_t *lds_idx = reinterpret_cast<const uint16_t *>(rtmi_bvh_lds + acc_s.nnodes + acc_s.nsph);
+    int32_t node = 0;
+    while (node < acc_s.nnodes) {
+      const uint4 nd = nodes[node];
+      const float tx0 = __builtin_fmaf(lo16(nd.x), ix, ox), tx1 = __builtin_fmaf(hi16(nd.x), ix, ox);
+      const float ty0 = __builtin_fmaf(lo16(nd.y), iy, oy), ty1 = __builtin_fmaf(hi16(nd.y), iy, oy);
+      const float tz0 = __builtin_fmaf(lo16(nd.z), iz, oz), tz1 = __builtin_fmaf(hi16(nd.z), iz, oz);
+      // slab interval clipped to [0, t_max].  No slack is needed: a sphere
+      // that can be hit lies >= the box margin inside the box, so its chord
+      // starts after tnear and ends before tfar by far more than rounding, and
+      // a hit at t_hit >= 0.001 with t_hit <= t_max (ties included) keeps the
+      // box entered.  Half-precision bounds only make the box larger.
+      const float tnear = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx0, tx1), __builtin_fminf(ty0, ty1)),
+                                          __builtin_fmaxf(__builtin_fminf(tz0, tz1), 0.0f));
+      const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx0, tx1), __builtin_fmaxf(ty0, ty1)),
+                                         __builtin_fminf(__builtin_fmaxf(tz0, tz1), t_max));
+      const bool enter = tnear <= tfar;
+      const int32_t link = int32_t(nd.w);
 #if RTMI_STATS
-    bstats[0] += 1;
-    if (__lane_id() == __builtin_ctzll(__ballot(1))) bstats[2] += 1;
+      bstats[0] += 1;
+      if (__lane_id() == __builtin_ctzll(__ballot(1))) bstats[2] += 1;
 #endif
-    if (enter && link < 0) {
-      const int32_t first = (~link) >> 4, cnt = (~link) & 15;
+      if (enter && link < 0) {
+        const int32_t first = (~link) >> 4, cnt = (~link) & 15;
 #if RTMI_STATS
-      bstats[1] += cnt;
+        bstats[1] += cnt;
 #endif
-      for (int32_t k = first; k < first + cnt; ++k) {
+        for (int32_t k = first; k < first + cnt; ++k) {
 #if RTMI_STATS
-        if (__lane_id() == __builtin_ctzll(__ballot(1))) bstats[3] += 1;
+          if (__lane_id() == __builtin_ctzll(__ballot(1))) bstats[3] += 1;
 #endif
-        float hb, disc;
-        sphere_test(lds_sph[k], d, K, a, aL, mx, my, mz, hb, disc);
-        if (!(disc < 0.0f)) {
+          float hb, disc;
+          sphere_test(sph[k], d, K, a, aL, mx, my, mz, hb, disc);
+          if (!(disc < 0.0f)) {
 #if RTMI_STATS
-          if (__lane_id() == __builtin_ctzll(__ballot(1))) bstats[4] += 1;
+            if (__lane_id() == __builtin_ctzll(__ballot(1))) bstats[4] += 1;
 #endif
-          resolve_root(int32_t(lds_idx[k]), hb, disc, inv_a, t_max, best);
+            resolve_root(GLOBAL ? acc_s.sph_idx[k] : int32_t(lds_idx[k]), hb, disc, inv_a, t_max, best);
+          }
         }
       }
+      node = (enter || link < 0) ? node + 1 : link;
     }
-    node = (enter || link < 0) ? node + 1 : link;
-  }
+  };
+  if (acc_s.bvh_global)
+    walk(std::true_type{});
+  else
+    walk(std::false_type{});
   t_hit = t_max;
   return best;
 }

@@ -263,6 +263,13 @@ __device__ __forceinline__ void flush_counters(const SegCounters &cnt, int lane,
 #endif
 }
 
+// Closest-hit kinds of the accelerated kernels (template ACC): 1 BVH, 2 the
+// uniform grid in LDS, 3 the same walked as one y layer, 4 / 5 the grid (one
+// layer) walked in global memory (a grid over the LDS budget)
+constexpr bool acc_grid(int A) { return A >= 2; }
+constexpr bool acc_flat(int A) { return A == 3 || A == 5; }
+constexpr bool acc_gmem(int A) { return A >= 4; }
+
 // One segment of a path — the body of the reference's recursive ray_color
 // (main.cpp:57-83) as one step of an iterative loop: the closest hit (brute
 // force, BVH or grid: the same hit bit for bit), then the sky of a miss,
@@ -291,7 +298,7 @@ __device__ __forceinline__ bool path_segment(const SceneView<float> &sc, const S
 #endif
     );
   } else if constexpr (ACC >= 2) {
-    k = hit_world_grid<kBigGroup, ACC == 3, FROM_BIG>(a.acc, o, d, t, key
+    k = hit_world_grid<kBigGroup, acc_flat(ACC), FROM_BIG, acc_gmem(ACC)>(a.acc, o, d, t, key
 #if RTMI_STATS
                                    , cnt.bvh_stats
 #endif
@@ -322,7 +329,9 @@ __device__ __forceinline__ bool path_segment(const SceneView<float> &sc, const S
   // slot (stage_grid): the hit record's geometry from there, one global
   // gather fewer (19.82 -> 19.73 ms, profiles/r03/ab_geom_lds.txt)
   const float4 sh1k = sc.sh1[kk], sh0k = sc.sh0[kk];
-  const float4 geomk = ACC >= 2 ? lds_sphere(key) : sc.geom[kk];
+  float4 geomk;
+  if constexpr (acc_gmem(ACC)) geomk = *reinterpret_cast<const float4 *>(a.acc.grid_gmem + key);
+  else geomk = ACC >= 2 ? lds_sphere(key) : sc.geom[kk];
   const int kind = miss ? -1 : int(sh1k.x);
   float inv_len = 0.0f;
   if (kind != RT_MAT_LAMBERTIAN) inv_len = drcp(dsqrt(dot<true>(d, d)));
@@ -386,6 +395,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   stage_camera(cam_lds, a);
   if constexpr (ACC == 0) __syncthreads();  // (accelerated kernels: stage_* ends with one)
   if constexpr (ACC == 1) stage_bvh(a.acc);  // block barrier inside: before any wave leaves
+  else if constexpr (acc_gmem(ACC)) stage_grid_desc(a.acc);
   else if constexpr (ACC >= 2) stage_grid(a.acc);
 #if RTMI_SYNC_PROBE
   const bool has_item = item < a.n_items;  // every wave stays for the per-pass block barriers
@@ -1323,6 +1333,7 @@ __global__ __launch_bounds__(256) void debug_hit_kernel(const SpherePair *__rest
                                                        const float *__restrict__ rays, int32_t n,
                                                        int32_t *__restrict__ out_idx, float *__restrict__ out_t) {
   if constexpr (ACC == 1) stage_bvh(acc);
+  else if constexpr (acc_gmem(ACC)) stage_grid_desc(acc);
   else stage_grid(acc);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -1333,14 +1344,14 @@ __global__ __launch_bounds__(256) void debug_hit_kernel(const SpherePair *__rest
 #if RTMI_STATS
   unsigned st[4] = {0, 0, 0, 0}, bst[5] = {0, 0, 0, 0, 0};
   out_idx[2 * i] = hit_world_packed<kPairGroup>(pairs, npairs, o, d, t0, st);
-  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1, bst) : hit_world_grid<kBigGroup, ACC == 3>(acc, o, d, t1, key, bst);
+  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1, bst) : hit_world_grid<kBigGroup, acc_flat(ACC), false, acc_gmem(ACC)>(acc, o, d, t1, key, bst);
 #else
   out_idx[2 * i] = hit_world_packed<kPairGroup>(pairs, npairs, o, d, t0);
 #if RTMI_TRACE_PHASES
   PhaseClock pc{{0, 0, 0}};
-  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup, ACC == 3>(acc, o, d, t1, key, pc);
+  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup, acc_flat(ACC), false, acc_gmem(ACC)>(acc, o, d, t1, key, pc);
 #else
-  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup, ACC == 3>(acc, o, d, t1, key);
+  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup, acc_flat(ACC), false, acc_gmem(ACC)>(acc, o, d, t1, key);
 #endif
 #endif
   out_t[2 * i] = t0;
@@ -1472,6 +1483,10 @@ struct rt_ctx {
   GridDesc grid{};
   int32_t ngrid_sph = 0;
   bool grid_ok = false;
+  bool grid_global = false;  // the grid is walked in global memory (grid_gmem: its LDS image)
+  char *grid_gmem = nullptr;
+  // RTMI_GRID_GLOBAL=1 (tests): the global-memory walk for any grid
+  bool force_grid_global = std::getenv("RTMI_GRID_GLOBAL") && std::atoi(std::getenv("RTMI_GRID_GLOBAL")) != 0;
   // cost-ordered dispatch: per-tile world.hit counts of the
   // last render with the same tile layout order the next one's tiles
   int32_t ordering = RT_ORDER_COST;
@@ -1617,7 +1632,8 @@ RTMI_EXPORT int rt_ctx_destroy(rt_ctx *ctx) {
                   (void *)ctx->sh164, (void *)ctx->accum, (void *)ctx->scratch, (void *)ctx->segments, (void *)ctx->pairs, (void *)ctx->counter, (void *)ctx->pass_accum,
                   (void *)ctx->big_pairs, (void *)ctx->big_idx, (void *)ctx->nodes, (void *)ctx->bvh_sph, (void *)ctx->bvh_idx,
                   (void *)ctx->cost_prev, (void *)ctx->cost_cur, (void *)ctx->cost_sorted, (void *)ctx->order,
-                  (void *)ctx->iota, ctx->sort_tmp, (void *)ctx->grid_sph, (void *)ctx->grid_cells, (void *)ctx->grid_refs})
+                  (void *)ctx->iota, ctx->sort_tmp, (void *)ctx->grid_sph, (void *)ctx->grid_cells, (void *)ctx->grid_refs,
+                  (void *)ctx->grid_gmem})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(ctx->stream);
   if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
@@ -1745,6 +1761,7 @@ struct GridBuild {
   std::vector<float4> sph;     // every sphere of the scene by scene index
   std::vector<uint32_t> cells;  // ncells + 1: each cell's first reference
   std::vector<uint32_t> refs;   // 16 x scene index
+  bool fits_lds = true;         // its LDS image fits the per-block budget (else: walked in global memory)
 };
 bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, int32_t n, int32_t nbig_slots,
                 GridBuild &out) {
@@ -1816,7 +1833,17 @@ bool build_grid(const BvhBuilder &b, const std::vector<int32_t> &small, int32_t 
   out.desc.nrefs = int32_t(out.refs.size());
   out.desc.cells_off = 16u * uint32_t(nbig_slots + out.desc.nrefs);  // grid_lds_bytes' layout
   out.desc.idx_off = out.desc.cells_off + 4u * uint32_t(out.desc.ncells + 1);
-  return grid_lds_bytes(nbig_slots, out.desc.ncells, out.desc.nrefs) <= kBvhLdsMax;
+  // The grid is staged in LDS only while a 4-wave block (its grid copy, one
+  // accumulator set, the static LDS) still leaves 8 blocks per CU; a larger
+  // one is walked in global memory (Accel::grid_gmem).  Measured
+  // (tools/large_scene_bench.py, profiles/r05/large/): the final scene's
+  // 17.6 KB grid 1.05 ms in LDS vs 1.13 in global memory (config 2: 19.2 vs
+  // 20.2 ms); 1 604 spheres (a 58 KB grid, 2 blocks per CU) 2.71 vs 1.13 ms.
+  // RTMI_GRID_LDS_MAX overrides the byte limit (A/B).
+  const char *lim_env = std::getenv("RTMI_GRID_LDS_MAX");
+  const size_t lds_max = lim_env && std::atoll(lim_env) > 0 ? size_t(std::atoll(lim_env)) : 160 * 1024 / 8 - 3 * 64 * 8 - 256;
+  out.fits_lds = grid_lds_bytes(nbig_slots, out.desc.ncells, out.desc.nrefs) <= lds_max;
+  return true;
 }
 }  // namespace
 
@@ -1971,6 +1998,25 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
       ctx->grid.cells = ctx->grid_cells;
       ctx->grid.refs = ctx->grid_refs;
       ctx->ngrid_sph = int32_t(gb.sph.size());
+      ctx->grid_global = ctx->force_grid_global || !gb.fits_lds;
+      if (ctx->grid_global) {
+        // the image stage_grid builds in LDS, offsets from 0: the slots (big
+        // spheres, then every cell's references as copies of their spheres'
+        // records), the cell starts, the slots' scene indices
+        const int32_t nbs = nb_pad, nrec = nbs + gb.desc.nrefs;
+        std::vector<char> img(grid_lds_bytes(nbs, gb.desc.ncells, gb.desc.nrefs), 0);
+        float4 *rec = reinterpret_cast<float4 *>(img.data());
+        uint32_t *cst = reinterpret_cast<uint32_t *>(img.data() + gb.desc.cells_off);
+        uint16_t *ix = reinterpret_cast<uint16_t *>(img.data() + gb.desc.idx_off);
+        for (int32_t i = 0; i < nrec; ++i) {
+          const int32_t k = i < nbs ? bidx[size_t(i)] : int32_t(gb.refs[size_t(i - nbs)] >> 4);  // dummies: -1
+          rec[i] = k < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : gb.sph[size_t(k)];
+          ix[i] = uint16_t(k < 0 ? 0 : k);
+        }
+        for (int32_t i = 0; i <= gb.desc.ncells; ++i) cst[i] = 16u * (uint32_t(nbs) + gb.cells[size_t(i)]);
+        if ((rc = dev_alloc(&ctx->grid_gmem, img.size()))) return rc;
+        HIP_TRY(hipMemcpy(ctx->grid_gmem, img.data(), img.size(), hipMemcpyHostToDevice));
+      }
       ctx->grid_ok = true;
     }
   }
@@ -2037,6 +2083,7 @@ namespace {
 
 size_t accel_lds_bytes(const Accel &acc, int kind) {
   if (kind == 1) return acc.bvh_global ? 0 : bvh_lds_bytes(acc.nnodes, acc.nsph);
+  if (kind >= 4) return 0;  // (the grid in global memory)
   if (kind >= 2) return grid_lds_bytes(2 * acc.nbig_pairs, acc.grid.ncells, acc.grid.nrefs);
   return 0;
 }
@@ -2056,6 +2103,7 @@ Accel accel_of(const rt_ctx *ctx, int kind) {
     a.sph = ctx->grid_sph;
     a.nsph = ctx->ngrid_sph;
     a.grid = ctx->grid;
+    a.grid_gmem = ctx->grid_global ? ctx->grid_gmem : nullptr;
   }
   return a;
 }
@@ -2121,6 +2169,8 @@ void launch_shape(bool persistent, int acc, bool chunked, dim3 grid, hipStream_t
     if (acc == 1) launch_tw<TW, 1>(chunked, grid, st, ctx, a, accum, out);
     else if (acc == 2) launch_tw<TW, 2>(chunked, grid, st, ctx, a, accum, out);
     else if (acc == 3) launch_tw<TW, 3>(chunked, grid, st, ctx, a, accum, out);
+    else if (acc == 4) launch_tw<TW, 4>(chunked, grid, st, ctx, a, accum, out);
+    else if (acc == 5) launch_tw<TW, 5>(chunked, grid, st, ctx, a, accum, out);
     else launch_tw<TW, 0>(chunked, grid, st, ctx, a, accum, out);
   }
 }
@@ -2176,11 +2226,11 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   // on config 2)
   // (a grid that does not fit, e.g. thousands of spheres, leaves the BVH)
   const int acc_kind = ctx->accel == RT_ACCEL_GRID && ctx->grid_ok
-                           ? (ctx->grid.n[1] == 1 ? 3 : 2)
+                           ? (ctx->grid.n[1] == 1 ? 3 : 2) + (ctx->grid_global ? 2 : 0)
                            : (ctx->accel != RT_ACCEL_NONE && ctx->nnodes > 0 ? 1 : 0);
   const bool bvh = acc_kind != 0;
   // the queue kernel: grid scenes, when selected
-  const bool queue = acc_kind >= 2 && ctx->kernel == RT_KERNEL_QUEUE && TW <= 16;
+  const bool queue = (acc_kind == 2 || acc_kind == 3) && ctx->kernel == RT_KERNEL_QUEUE && TW <= 16;
   const int64_t qblocks = queue ? queue_resident_blocks(ctx, accel_lds_bytes(accel_of(ctx, acc_kind), acc_kind)) : 0;
   // the persistent kernel runs brute-force scenes only (see the note above stage_camera)
   const bool persistent = !bvh && (ctx->kernel == RT_KERNEL_PERSISTENT ||
@@ -2259,7 +2309,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   const bool chunked = pass_accum || nch1 + nch2 > 1;
   if (!ctx->probing) {
     const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush + a.block_owns_tile, persistent ? 0 : 1,
-                              queue ? 2 : (persistent ? 1 : 0), acc_kind == 3 ? 2 : acc_kind};
+                              queue ? 2 : (persistent ? 1 : 0), acc_kind == 3 ? 2 : (acc_kind == 5 ? 4 : acc_kind)};
     std::copy(sched, sched + 8, ctx->last_sched);
   }
   a.s_base = s_base;
@@ -2717,7 +2767,9 @@ RTMI_EXPORT int rt_ctx_debug_hits(rt_ctx *ctx, const float *rays, int32_t n, int
     return rc;
   HIP_TRY(hipMemcpy(d_rays, rays, size_t(n) * 6 * sizeof(float), hipMemcpyHostToDevice));
   // the walk the renders use (3: the one-layer grid walk)
-  const int kind = ctx->accel == RT_ACCEL_GRID ? (ctx->grid_ok && ctx->grid.n[1] == 1 ? 3 : 2) : 1;
+  const int kind = ctx->accel == RT_ACCEL_GRID
+                       ? (ctx->grid_ok && ctx->grid.n[1] == 1 ? 3 : 2) + (ctx->grid_ok && ctx->grid_global ? 2 : 0)
+                       : 1;
   if ((kind == 1 && !ctx->nnodes) || (kind >= 2 && !ctx->grid_ok)) {
     (void)hipFree(d_rays); (void)hipFree(d_idx); (void)hipFree(d_t);
     return set_error(RT_EUNSUPPORTED, "rt_ctx_debug_hits: no %s for this scene", kind >= 2 ? "grid" : "BVH");
@@ -2730,8 +2782,14 @@ RTMI_EXPORT int rt_ctx_debug_hits(rt_ctx *ctx, const float *rays, int32_t n, int
   else if (kind == 2)
     hipLaunchKernelGGL(debug_hit_kernel<2>, dim3(unsigned((n + 255) / 256)), dim3(256), lds, ctx->stream, ctx->pairs,
                        ctx->npairs, acc, d_rays, n, d_idx, d_t);
-  else
+  else if (kind == 3)
     hipLaunchKernelGGL(debug_hit_kernel<3>, dim3(unsigned((n + 255) / 256)), dim3(256), lds, ctx->stream, ctx->pairs,
+                       ctx->npairs, acc, d_rays, n, d_idx, d_t);
+  else if (kind == 4)
+    hipLaunchKernelGGL(debug_hit_kernel<4>, dim3(unsigned((n + 255) / 256)), dim3(256), lds, ctx->stream, ctx->pairs,
+                       ctx->npairs, acc, d_rays, n, d_idx, d_t);
+  else
+    hipLaunchKernelGGL(debug_hit_kernel<5>, dim3(unsigned((n + 255) / 256)), dim3(256), lds, ctx->stream, ctx->pairs,
                        ctx->npairs, acc, d_rays, n, d_idx, d_t);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));

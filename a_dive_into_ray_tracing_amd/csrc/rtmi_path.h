@@ -464,6 +464,9 @@ struct Accel {
   int32_t nsph;              // float4s of sph
   GridDesc grid;             // RT_ACCEL_GRID only
   int32_t bvh_global;        // BVH too large for LDS: walked in global memory (L2)
+  // a grid over the LDS budget: the image stage_grid builds in LDS (slots,
+  // cell starts, indices; offsets from 0) in global memory
+  const char *grid_gmem;
 };
 
 // big_idx through the constant address space: wave-uniform scalar loads
@@ -543,6 +546,12 @@ __device__ __forceinline__ void stage_grid(const Accel &g) {
   }
   for (int i = threadIdx.x; i <= g.grid.ncells; i += blockDim.x)
     c[i] = rec_base + 16u * (uint32_t(nbs) + g.grid.cells[i]);
+  __syncthreads();
+}
+// A grid walked in global memory (Accel::grid_gmem): only the descriptor is
+// staged; slots, cell starts and indices are read at gmem + the same offsets.
+__device__ __forceinline__ void stage_grid_desc(const Accel &g) {
+  if (threadIdx.x == 0) rtmi_grid_desc = g.grid;
   __syncthreads();
 }
 // a uint32 at an LDS address
@@ -629,18 +638,23 @@ __device__ __forceinline__ void resolve_root(int32_t idx, float hb, float disc, 
 // (stage_grid): the same acceptance, with the scene indices read from the
 // slot index table only for an exact tie (r == t_max), which is rare, instead
 // of carried per candidate.  best_key -1: no hit yet.
+template <bool GMEM = false>
 __device__ __forceinline__ void resolve_key(uint32_t key, float hb, float disc, float inv_a, float &t_max,
-                                            int32_t &best_key, uint32_t idx_base) {
+                                            int32_t &best_key, uint32_t idx_base, const char *gmem = nullptr) {
   const float sq = dsqrt(disc);
   const float r1 = (-hb - sq) * inv_a, r2 = (-hb + sq) * inv_a;
   const bool g1 = !(r1 < 0.001f), g2 = !(r2 < 0.001f);
   bool ok1 = g1 & (r1 < t_max), ok2 = g2 & (r2 < t_max);
   const bool e1 = g1 & (r1 == t_max), e2 = g2 & (r2 == t_max);
   if (__builtin_expect(e1 | e2, 0)) {
-    const uint32_t rec_base = lds_address(rtmi_bvh_lds);
+    const uint32_t rec_base = GMEM ? 0u : lds_address(rtmi_bvh_lds);
     const uint32_t bk = best_key < 0 ? key : uint32_t(best_key);
-    const bool later = (best_key < 0) | (lds_u16(idx_base + ((key - rec_base) >> 3)) >
-                                         lds_u16(idx_base + ((bk - rec_base) >> 3)));
+    auto u16 = [&](uint32_t a) {
+      if constexpr (GMEM) return uint32_t(*reinterpret_cast<const uint16_t *>(gmem + a));
+      else return lds_u16(a);
+    };
+    const bool later = (best_key < 0) | (u16(idx_base + ((key - rec_base) >> 3)) >
+                                         u16(idx_base + ((bk - rec_base) >> 3)));
     ok1 |= e1 & later;
     ok2 |= e2 & later;
   }
@@ -654,7 +668,7 @@ __device__ __forceinline__ void resolve_key(uint32_t key, float hb, float disc, 
 // and the r = 1 spheres) by the packed brute-force loop: group data and scene
 // indices through scalar loads, each half of a v_pk_fma_f32 an IEEE fma.
 // KEYS (the grid walk): best is a record-slot key, slot j's key rec_base + 16 j.
-template <int GP, bool KEYS = false>
+template <int GP, bool KEYS = false, bool GMEM = false>
 __device__ __forceinline__ void hit_big(const Accel &acc_s, V3<float> d, float K, float a, float aL, float mx, float my,
                                         float mz, float inv_a, float &t_max, int32_t &best
 #if RTMI_STATS
@@ -691,7 +705,8 @@ __device__ __forceinline__ void hit_big(const Accel &acc_s, V3<float> d, float K
 #endif
       auto res = [&](int slot, float hb, float disc) {
         if constexpr (KEYS)  // the big slots' keys are in scene order: the plain tie rule
-          resolve_root(int32_t(lds_address(rtmi_bvh_lds) + 16u * uint32_t(slot)), hb, disc, inv_a, t_max, best);
+          resolve_root(int32_t((GMEM ? 0u : lds_address(rtmi_bvh_lds)) + 16u * uint32_t(slot)), hb, disc, inv_a, t_max,
+                       best);
         else
           resolve_root(big_index(acc_s, slot), hb, disc, inv_a, t_max, best);
       };
@@ -723,7 +738,7 @@ __device__ __forceinline__ void hit_big(const Accel &acc_s, V3<float> d, float K
 // FROM_BIG (the queue kernel): the big spheres' pass was run
 // when the ray was made (grid_big): the walk starts from its result, given in
 // t_max0 / best0.
-template <int GP, bool FLAT_Y = false, bool FROM_BIG = false>
+template <int GP, bool FLAT_Y = false, bool FROM_BIG = false, bool GMEM = false>
 __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> o, V3<float> d, float &t_hit,
                                                   uint32_t &hit_key
 #if RTMI_STATS
@@ -740,11 +755,25 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
   // the record slots (grid_lds_bytes); the slot index table's address from
   // the kernel arguments, a scalar (from the LDS descriptor it would be a
   // VGPR held through the walk, which the kernel has none to spare of)
-  const uint32_t base = lds_address(rtmi_bvh_lds), idx_base = base + acc_s.grid.idx_off;
+  // (GMEM: the same layout in global memory at acc_s.grid_gmem, offsets from 0)
+  const char *const gm = GMEM ? acc_s.grid_gmem : nullptr;
+  const uint32_t base = GMEM ? 0u : lds_address(rtmi_bvh_lds), idx_base = base + acc_s.grid.idx_off;
+  auto rd_u32 = [&](uint32_t addr) {
+    if constexpr (GMEM) return *reinterpret_cast<const uint32_t *>(gm + addr);
+    else return lds_u32(addr);
+  };
+  auto rd_u16 = [&](uint32_t addr) {
+    if constexpr (GMEM) return uint32_t(*reinterpret_cast<const uint16_t *>(gm + addr));
+    else return lds_u16(addr);
+  };
+  auto rd_sphere = [&](uint32_t addr) {
+    if constexpr (GMEM) return *reinterpret_cast<const float4 *>(gm + addr);
+    else return lds_sphere(addr);
+  };
   float t_max = t_max0;
   int32_t best_a = best0;  // the hit's record-slot key; -1: no hit yet
   if constexpr (!FROM_BIG)
-    hit_big<GP, true>(acc_s, d, K, a, aL, mx, my, mz, inv_a, t_max, best_a
+    hit_big<GP, true, GMEM>(acc_s, d, K, a, aL, mx, my, mz, inv_a, t_max, best_a
 #if RTMI_STATS
                 , gstats
 #endif
@@ -812,7 +841,7 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
       gstats[0] += 1;
       if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[2] += 1;
 #endif
-      const uint32_t re = lds_u32(cell + 4u);  // (with the next one: a ds_read2_b32)
+      const uint32_t re = rd_u32(cell + 4u);  // (with the next one: a ds_read2_b32)
       // Deferred root resolution: a lane keeps its first candidate of the
       // cell and resolves it after the cell's sphere loop (a second candidate
       // resolves the kept one first).  A wave then runs the resolution about
@@ -826,19 +855,19 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
       constexpr uint32_t kNoKey = 0xFFFFFFFFu;
       uint32_t kaddr = kNoKey;
       float khb = 0.0f, kdisc = 0.0f;
-      for (uint32_t r = lds_u32(cell); r < re; r += 16u) {
+      for (uint32_t r = rd_u32(cell); r < re; r += 16u) {
 #if RTMI_STATS
         gstats[1] += 1;
         if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[3] += 1;
 #endif
         float hb, disc;
-        sphere_test(lds_sphere(r), d, K, a, aL, mx, my, mz, hb, disc);
+        sphere_test(rd_sphere(r), d, K, a, aL, mx, my, mz, hb, disc);
         if (!(disc < 0.0f)) {
           if (kaddr != kNoKey) {
 #if RTMI_STATS
             if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
 #endif
-            resolve_key(kaddr, khb, kdisc, inv_a, t_max, best_a, idx_base);
+            resolve_key<GMEM>(kaddr, khb, kdisc, inv_a, t_max, best_a, idx_base, gm);
           }
           kaddr = r;
           khb = hb;
@@ -849,7 +878,7 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
 #if RTMI_STATS
         if (__lane_id() == __builtin_ctzll(__ballot(1))) gstats[4] += 1;
 #endif
-        resolve_key(kaddr, khb, kdisc, inv_a, t_max, best_a, idx_base);
+        resolve_key<GMEM>(kaddr, khb, kdisc, inv_a, t_max, best_a, idx_base, gm);
       }
       const float texit = __builtin_fminf(tnx, __builtin_fminf(tny, tnz));
       if constexpr (FLAT_Y) {
@@ -896,7 +925,7 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
   t_hit = t_max;
   // the scene index of the hit slot (a miss reads slot 0's, unused)
   hit_key = best_a < 0 ? base : uint32_t(best_a);
-  const int32_t k = int32_t(lds_u16(idx_base + ((hit_key - base) >> 3)));
+  const int32_t k = int32_t(rd_u16(idx_base + ((hit_key - base) >> 3)));
   return best_a < 0 ? -1 : k;
 }
 

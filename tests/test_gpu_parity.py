@@ -962,6 +962,47 @@ def test_config3_strips_unpermute_to_config2_frame(G, config2, final_world):
     assert np.array_equal(rdist.unpermute(strips, H), img)
 
 
+def test_concurrent_contexts_with_different_scenes_and_paths():
+    """Contexts run concurrently on their own streams (as bench.py's two
+    contexts do), here with different scenes and closest-hit paths at once:
+    the final scene through the LDS grid, the learn scene brute force, and a
+    2 000-sphere scene through the grid in global memory, each launched
+    several times back to back without synchronising; every image equals its
+    oracle render."""
+    torch = pytest.importorskip("torch")
+    g = np.random.default_rng(5)
+    n = 2000
+    c = np.column_stack([g.uniform(-20, 20, n), np.full(n, 0.2), g.uniform(-20, 20, n)])
+    kinds = g.integers(0, 3, n).astype(np.int32)
+    params = np.column_stack([g.uniform(0.1, 0.9, (n, 3)), np.where(kinds == 2, 1.5, g.uniform(0, 0.5, n))])
+    big = rt.World(np.vstack([[0, -1000, 0, 1000], np.column_stack([c, np.full(n, 0.2)])]),
+                   np.concatenate([[0], kinds]).astype(np.int32), np.vstack([[0.5, 0.5, 0.5, 0], params]))
+    W, H, S = 40, 24, 8
+    jobs = [(rt.random_scene(), rt.final_camera(W / H), "grid"), (rt.learn_scene(), rt.learn_camera(W / H), "none"),
+            (big, rt.camera((20, 3, 12), (0, 0, 0), (0, 1, 0), 30.0, W / H, 0.05, 20.0), "grid")]
+    rs, outs, streams = [], [], []
+    try:
+        for world, cam, accel in jobs:
+            r = rt.Renderer(world, 0)
+            r.set_accel(accel)
+            rs.append(r)
+            streams.append(torch.cuda.Stream("cuda:0"))
+            outs.append([torch.full((H, W, 3), -1.0, dtype=torch.float32, device="cuda:0") for _ in range(3)])
+        for k in range(3):
+            for i, (world, cam, _) in enumerate(jobs):
+                rs[i].render_rows(cam, W, H, S, 50, SEED, 0, 1, H, outs[i][k].data_ptr(), streams[i].cuda_stream)
+        torch.cuda.synchronize()
+        paths = [r.last_schedule()["bvh"] for r in rs]
+    finally:
+        for r in rs:
+            r.close()
+    assert paths == [2, 0, 4], paths
+    for i, (world, cam, _) in enumerate(jobs):
+        want = O.fast_render(o_scene(world), o_cam(cam), W, H, S, 50, SEED)
+        for k in range(3):
+            assert np.array_equal(outs[i][k].cpu().numpy(), want), (i, k)
+
+
 def test_overlapped_contexts_strips_equal_frame(config2, final_world):
     """bench.py --pipeline 2: two contexts with the overlap hint
     (rt_ctx_set_overlap: fewer, longer work items) render the 8 strips of

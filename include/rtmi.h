@@ -161,9 +161,11 @@ int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind);
  * reports the split (big spheres, BVH nodes) of the current scene.
  * RT_ACCEL_GRID: the same split, the small spheres in a uniform grid walked
  * by a 3D DDA; same closest hit bit for bit.
- * rt_ctx_grid_info reports its cells per axis, references and LDS bytes
- * (RT_EUNSUPPORTED when the scene has no grid: the render then uses brute
- * force). */
+ * rt_ctx_grid_info reports its cells per axis, references and image bytes
+ * (RT_EUNSUPPORTED when the scene has no grid — over 65 535 spheres: the
+ * render then uses the BVH).  Each structure is staged in LDS per block when
+ * it fits; a larger one (scenes of thousands of spheres) is walked in global
+ * memory — the same hits. */
 enum { RT_ACCEL_NONE = 0, RT_ACCEL_BVH = 1, RT_ACCEL_GRID = 2 };
 /* (a new context starts with RT_ACCEL_GRID: same image as brute force, and
  * the fastest on the reference's scenes — DESIGN.md §4.4) */

@@ -1977,12 +1977,18 @@ RTMI_EXPORT int rt_ctx_set_scene(rt_ctx *ctx, const rt_scene *scene) {
     ctx->nbig = int32_t(big.size());
     ctx->nbig_pairs = nb_pad / 2;
     ctx->nbvh_sph = int32_t(b.sph.size());
-    // the BVH is staged in LDS when it fits the budget beside the
-    // accumulators (and its 16-bit scene indices suffice); a larger one is
-    // walked in global memory (L2), still far fewer tests than brute force
+    // the BVH is staged in LDS while a block (BVH, one accumulator set, the
+    // static LDS) still leaves 8 blocks per CU and its 16-bit scene indices
+    // suffice; a larger one is walked in global memory (L2).  Measured
+    // (profiles/r05/large/threshold_ab.txt): 488 spheres 1.90 ms in LDS vs
+    // 2.06 global, 904 spheres 2.33 vs 2.34, 1 604 spheres 3.74 vs 2.42.
+    // RTMI_BVH_LDS_MAX overrides the byte limit (A/B).
     const size_t lds = bvh_lds_bytes(int32_t(b.nodes.size()), int32_t(b.sph.size()));
+    const char *lim_env = std::getenv("RTMI_BVH_LDS_MAX");
+    const size_t lds_max = lim_env && std::atoll(lim_env) > 0 ? std::min<size_t>(kBvhLdsMax, size_t(std::atoll(lim_env)))
+                                                             : 160 * 1024 / 8 - 3 * 64 * 8 - 256;
     ctx->nnodes = int32_t(b.nodes.size());
-    ctx->bvh_global = ctx->force_bvh_global || !(lds <= kBvhLdsMax && n <= 65535);
+    ctx->bvh_global = ctx->force_bvh_global || !(lds <= lds_max && n <= 65535);
     // uniform grid over the same small spheres
     ctx->grid_ok = false;
     GridBuild gb;

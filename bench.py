@@ -605,7 +605,11 @@ def main():
         x.set_kernel(args.kernel)
         x.set_accel(args.accel)
         x.set_ordering(args.ordering)
-        if npipe > 1:  # the launches of the two contexts overlap: fewer, longer items (rt_ctx_set_overlap)
+        # the launches of the two contexts overlap: fewer, longer items
+        # (rt_ctx_set_overlap) — from 8 timed steps up; in shorter runs the
+        # last launch's longer drain is shared by too few steps (1/8 strip at
+        # K = 5: 2.81 vs 2.74 ms; K = 10: 2.65 vs 2.70; profiles/r05/pipeline/ab_items_short.txt)
+        if npipe > 1 and args.steps >= 8:
             x.set_overlap(True)
         return x
 
@@ -926,6 +930,7 @@ def main():
                 "accel": args.accel,
                 "ordering": args.ordering,
                 "pipeline": npipe,
+                "overlap_schedule": bool(npipe > 1 and args.steps >= 8 and not STUB),
                 "timed_steps": ("each step re-renders the same workload; with ordering 'cost' it dispatches tiles by the "
                                 "previous identical render's per-tile cost map (RT_ORDER_COST): the first render of a "
                                 "layout (warmup) pays a 1-2 spp probe pass instead, see one_shot_msamples_per_s"

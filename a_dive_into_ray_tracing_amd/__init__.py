@@ -191,7 +191,7 @@ class Renderer:
         the same device (rt_ctx_set_overlap); fewer, longer work items."""
         check(self.L.rt_ctx_set_overlap(self._h, int(bool(overlapped))), "rt_ctx_set_overlap")
 
-    KERNELS = {"grid": 0, "persistent": 1, "auto": 2, "queue": 3}  # RT_KERNEL_* (include/rtmi.h)
+    KERNELS = {"grid": 0, "persistent": 1, "auto": 2, "queue": 3, "resident": 4}  # RT_KERNEL_* (include/rtmi.h)
 
     def set_kernel(self, kind="auto"):
         check(self.L.rt_ctx_set_kernel(self._h, self.KERNELS[kind]), "rt_ctx_set_kernel")

@@ -158,6 +158,7 @@ SIGNATURES = {
     "rt_nw_ctx_last_segments": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     "rt_nw_ctx_last_kernel": (C.c_int, [C.c_void_p, _ip]),
     "rt_nw_debug_trace": (C.c_int, [C.c_void_p, C.POINTER(RtNwCamera)] + [C.c_int32] * 3 + [C.c_uint64] + [C.c_int32] * 3 + [_fp, C.c_int32, _ip]),
+    "rt_nw_debug_hits": (C.c_int, [C.c_void_p, _fp, C.POINTER(C.c_uint64), C.c_int32, _ip, _fp, _ip]),
 }
 
 _lib = None

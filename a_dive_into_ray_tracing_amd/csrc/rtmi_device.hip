@@ -131,6 +131,11 @@ __device__ unsigned g_trace_n;
 #ifndef RTMI_SYNC_PROBE
 #define RTMI_SYNC_PROBE 0
 #endif
+// analysis only (A/B): work items numbered chunk-major, so a grid-kernel
+// block's waves render four different tiles (what tile locality is worth)
+#ifndef RTMI_CHUNK_MAJOR
+#define RTMI_CHUNK_MAJOR 0
+#endif
 #ifndef RTMI_PAIR_GROUP
 #define RTMI_PAIR_GROUP 4
 #endif
@@ -406,8 +411,13 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
 
   auto item_range = [&](int it, int &tl, int &sb, int &n) {
     if (it < a.tiles * a.nch1) {
+#if RTMI_CHUNK_MAJOR  // analysis only: a block's waves on different tiles (block_flush off)
+      tl = it % a.tiles;
+      sb = (it / a.tiles) * a.chunk1;
+#else
       tl = it / a.nch1;
       sb = (it - tl * a.nch1) * a.chunk1;
+#endif
       n = max(0, min(a.chunk1, a.spp1 - sb));  // 0: an empty item of the automatic schedule
     } else {
       const int i2 = it - a.tiles * a.nch1;
@@ -633,6 +643,295 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
       else out[o3 + c] = from_fixed((long long)v);
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// resident grid kernel (RT_KERNEL_RESIDENT)
+// ---------------------------------------------------------------------------
+// render_kernel's per-wave loop in CU-resident blocks: each wave takes work
+// items from a global counter until none is left, with its own fixed-point
+// sums in LDS, flushed (global atomics, or the floats when the item covers
+// all samples of its tile) at the end of every item.  No wave waits for
+// another: render_kernel's 4-wave block holds its wave slots until its
+// slowest wave ends, and a launch drains as those blocks do (one rank's 1/8
+// strip of config 2: 86-93% of the 8 192 wave slots resident mid-run, the
+// slots emptying over the last ~30% of the launch).  Here every
+// slot stays busy until the counter runs out, and the tail is each wave's
+// last item.  Blocks of kResWaves waves stage the structure once (two copies
+// per CU instead of eight).  Same per-path arithmetic (path_segment) and
+// integer sums: the image is bit-identical to every other kernel's.
+#ifndef RTMI_RES_WAVES
+#define RTMI_RES_WAVES 16
+#endif
+constexpr int kResWaves = RTMI_RES_WAVES;
+// analysis variants (A/B only, never the product): RTMI_RES_NOFLUSH=1 skips
+// the flush's global writes (wrong image: what the flush costs),
+// RTMI_RES_STATIC=1 assigns items round-robin instead of by the counter
+#ifndef RTMI_RES_NOFLUSH
+#define RTMI_RES_NOFLUSH 0
+#endif
+#ifndef RTMI_RES_STATIC
+#define RTMI_RES_STATIC 0
+#endif
+// RTMI_RES_TEAM=1 (analysis): waves 4t..4t+3 of a block (one per SIMD) take
+// the four items of one tile together, as a grid-kernel block does — the
+// team's first wave at round r claims the tile group, the others read it
+// from an LDS ring (no overflow protection: A/B only)
+#ifndef RTMI_RES_TEAM
+#define RTMI_RES_TEAM 0
+#endif
+static_assert(kResWaves >= 1 && kResWaves <= 16, "a block holds at most 16 waves");
+
+template <int TW, int ACC>
+__global__ __launch_bounds__(64 * kResWaves, 8) void render_resident(
+    const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1,
+    RenderArgs a, unsigned long long *__restrict__ accum, float *__restrict__ out,
+    unsigned long long *__restrict__ segments, unsigned *__restrict__ counter) {
+  static_assert(ACC >= 1, "accelerated scenes only (brute force: render_persistent)");
+  constexpr int TH = 64 / TW;
+  __shared__ float cam_lds[21];  // the camera (stage_camera)
+  // The arguments the item decode and the flush read, in LDS: read there
+  // once per item instead of held in scalar registers through the path
+  // loop (held, they spilled 45 scalar registers into VGPR lanes and 2-14
+  // VGPRs to scratch)
+  enum { kTiles, kNch1, kChunk1, kSpp1, kNch2, kChunk2, kSpp, kTilesX, kW, kRows, kNItems, kOwns, kFirst,
+         kOrder, kCost = kOrder + 2, kAccum = kCost + 2, kOut = kAccum + 2, kCounter = kOut + 2,
+         kSegs = kCounter + 2, kArgs = kSegs + 2 };
+  __shared__ uint32_t args_lds[kArgs];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x == 0) {
+    const int32_t v[kFirst + 1] = {a.tiles, a.nch1, a.chunk1, a.spp1, a.nch2, a.chunk2, a.spp, a.tiles_x, a.W,
+                                   a.nrows_valid, a.n_items, a.block_owns_tile, int32_t(gridDim.x) * kResWaves};
+    for (int i = 0; i <= kFirst; ++i) args_lds[i] = uint32_t(v[i]);
+    auto ptr = [&](int at, const void *p) {
+      args_lds[at] = uint32_t(size_t(p));
+      args_lds[at + 1] = uint32_t(size_t(p) >> 32);
+    };
+    ptr(kOrder, a.tile_order);
+    ptr(kCost, a.tile_cost);
+    ptr(kAccum, accum);
+    ptr(kOut, out);
+    ptr(kCounter, counter);
+    ptr(kSegs, segments);
+  }
+  // (read after a workgroup fence, so not hoisted out of the item loop)
+  auto arg = [&](int i) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    return int(__builtin_amdgcn_readfirstlane(int(args_lds[i])));
+  };
+  auto arg_ptr = [&](int i) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const uint32_t lo = uint32_t(__builtin_amdgcn_readfirstlane(int(args_lds[i])));
+    const uint32_t hi = uint32_t(__builtin_amdgcn_readfirstlane(int(args_lds[i + 1])));
+    return reinterpret_cast<void *>((size_t(hi) << 32) | lo);
+  };
+  // this wave's sums [3][64], in the dynamic LDS past the structure; zeroed
+  // before the staging barrier, which publishes them, and again by every flush
+  unsigned long long *const acc =
+      reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(rtmi_bvh_lds) + a.acc_off) + wave * 3 * 64;
+  for (int c = 0; c < 3; ++c) acc[64 * c + lane] = 0;
+  stage_camera(cam_lds, a);
+  if constexpr (ACC == 1) stage_bvh(a.acc);  // (each ends with the block barrier)
+  else if constexpr (acc_gmem(ACC)) stage_grid_desc(a.acc);
+  else stage_grid(a.acc);
+
+  const SceneView<float> sc{geom, sh0, sh1, a.n};
+  SegCounters cnt{};
+  RTMI_TRACE_BEGIN
+#if RTMI_TRACE
+  unsigned wsegs = 0;
+  int items_done = 0;
+#endif
+  auto pull = [](int src4, float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(src4, __float_as_int(v))); };
+  auto pull64 = [](int src4, uint64_t v) {
+    const uint32_t lo = uint32_t(__builtin_amdgcn_ds_bpermute(src4, int(uint32_t(v))));
+    const uint32_t hi = uint32_t(__builtin_amdgcn_ds_bpermute(src4, int(uint32_t(v >> 32))));
+    return (uint64_t(hi) << 32) | lo;
+  };
+  // the first item by position, the next ones from the counter (which the
+  // host zeroes: items past the grid's first gridDim.x * kResWaves)
+#if RTMI_RES_TEAM
+  __shared__ uint32_t team_round[kResWaves / 4];
+  __shared__ unsigned long long team_ring[kResWaves / 4][64];
+  if (threadIdx.x < kResWaves / 4) team_round[threadIdx.x] = 0;
+  if (threadIdx.x < kResWaves / 4 * 64) (&team_ring[0][0])[threadIdx.x] = ~0ull;
+  __syncthreads();
+  uint32_t round = 0;
+  auto team_item = [&]() {
+    const int t = wave >> 2;
+    unsigned long long v = 0;
+    if (lane == 0) {
+      if (atomicCAS(&team_round[t], round, round + 1) == round) {
+        const unsigned g = atomicAdd(static_cast<unsigned *>(arg_ptr(kCounter)), 1u);
+        v = (uint64_t(round) << 32) | g;
+        __hip_atomic_store(&team_ring[t][round & 63], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+        for (;;) {
+          v = __hip_atomic_load(&team_ring[t][round & 63], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (uint32_t(v >> 32) == round) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+    }
+    ++round;
+    return 4 * __builtin_amdgcn_readfirstlane(int(uint32_t(v))) + (wave & 3);
+  };
+  int item = team_item();
+#else
+  int item = blockIdx.x * kResWaves + wave;
+#endif
+  while (item < arg(kNItems)) {
+    int tile, s0, ns;
+    {
+      const int tiles = arg(kTiles), nch1 = arg(kNch1), chunk1 = arg(kChunk1);
+      if (item < tiles * nch1) {
+        tile = item / nch1;
+        s0 = (item - tile * nch1) * chunk1;
+        ns = max(0, min(chunk1, arg(kSpp1) - s0));
+      } else {
+        const int nch2 = arg(kNch2), chunk2 = arg(kChunk2);
+        const int i2 = item - tiles * nch1;
+        tile = i2 / nch2;
+        s0 = arg(kSpp1) + (i2 - tile * nch2) * chunk2;
+        ns = max(0, min(chunk2, arg(kSpp) - s0));
+      }
+      const int32_t *order = static_cast<const int32_t *>(arg_ptr(kOrder));
+      if (order) tile = order[tile];  // expensive tiles first
+    }
+    tile = __builtin_amdgcn_readfirstlane(tile);
+    const int tiles_x = arg(kTilesX);
+    const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+    const int x0 = tx * TW, y0 = ty * TH;
+    const int vw = min(TW, a.W - x0), vh = min(TH, arg(kRows) - y0);
+    const int nv = vw * vh;
+    const int nq = nv * ns;
+    unsigned nseg = 0;
+
+    // the per-wave loop of render_kernel (path regeneration from the
+    // camera-ray pool; see there)
+    V3<float> o, d, T;
+    int pxd = 0;
+    bool active = true;
+    Xoro rng;
+    const uint32_t m_nv = 0x7FFFFFFFu / uint32_t(max(nv, 1)) + 1u, m_vw = 0x7FFFFFFFu / uint32_t(vw) + 1u;
+    auto camera_ray = [&](int q, V3<float> &ro, V3<float> &rd, Xoro &g) {
+      const int qs = int(__umulhi(uint32_t(q) << 1, m_nv));
+      const int s = s0 + qs;
+      const int p = q - qs * nv;
+      const int ly = int(__umulhi(uint32_t(p) << 1, m_vw)), lx = p - ly * vw;
+      const int i = x0 + lx;
+      const int j = a.row0 + (y0 + ly) * a.row_step;
+      g.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(a.s_base + s));
+      float ju, jv;
+      g.pair(ju, jv);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // camera read here, not hoisted out of the loop
+      const float u = (float(i) + ju) * cam_lds[19];  // main.cpp:278, by the reciprocal
+      const float v = (float(j) + jv) * cam_lds[20];  // main.cpp:279
+      get_ray<true, float>(lds_camera(cam_lds), u, v, g, ro, rd);
+    };
+    auto adopt = [&](int q, const V3<float> &ro, const V3<float> &rd, const Xoro &g) {
+      if (q < nq) {
+        o = ro;
+        d = rd;
+        rng = g;
+        pxd = (q - int(__umulhi(uint32_t(q) << 1, m_nv)) * nv) << 24;
+        T = mk(1.f, 1.f, 1.f);
+      } else {
+        active = false;
+      }
+    };
+    V3<float> po, pd;
+    Xoro prng;
+    int pbase = 0, ppos = 64;
+    camera_ray(lane, po, pd, prng);
+    adopt(lane, po, pd, prng);
+    for (;;) {
+      const unsigned long long live = __ballot(active);
+      if (live == 0) break;
+      nseg = unsigned(__builtin_amdgcn_readfirstlane(int(nseg + unsigned(__popcll(live)))));
+      bool done = false;
+      V3<float> col = mk(0.f, 0.f, 0.f);
+      if (active) done = path_segment<ACC>(sc, nullptr, a, o, d, T, pxd, rng, col, cnt, segments);
+      const unsigned long long m = __ballot(done);
+      if (m) {
+        if (done) {
+          const int px = pxd >> 24;
+          atomicAdd(&acc[px], (unsigned long long)to_fixed(col.x));
+          atomicAdd(&acc[64 + px], (unsigned long long)to_fixed(col.y));
+          atomicAdd(&acc[128 + px], (unsigned long long)to_fixed(col.z));
+        }
+        const int rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
+        const int cnt_done = __popcll(m);
+        for (int served = 0; served < cnt_done;) {
+          if (ppos == 64) {
+            pbase = __builtin_amdgcn_readfirstlane(pbase + 64);
+            ppos = 0;
+            if (pbase < nq) camera_ray(pbase + lane, po, pd, prng);
+          }
+          const int take = min(cnt_done - served, 64 - ppos);
+          const int r = rank - served;
+          const int src4 = ((ppos + r) & 63) << 2;
+          V3<float> ro, rd;
+          Xoro g;
+          ro = mk(pull(src4, po.x), pull(src4, po.y), pull(src4, po.z));
+          rd = mk(pull(src4, pd.x), pull(src4, pd.y), pull(src4, pd.z));
+          g.s0 = pull64(src4, prng.s0);
+          g.s1 = pull64(src4, prng.s1);
+          if (done && r >= 0 && r < take) adopt(pbase + ppos + r, ro, rd, g);
+          ppos = __builtin_amdgcn_readfirstlane(ppos + take);
+          served = __builtin_amdgcn_readfirstlane(served + take);
+        }
+      }
+    }
+    // the next item's claim first: its latency overlaps the flush
+    unsigned next = 0;
+    if (lane == 0) {
+#if RTMI_RES_STATIC
+      next = unsigned(item);
+#elif RTMI_RES_TEAM
+      next = 0;
+#else
+      next = atomicAdd(static_cast<unsigned *>(arg_ptr(kCounter)), 1u);
+#endif
+      atomicAdd(static_cast<unsigned long long *>(arg_ptr(kSegs)), (unsigned long long)nseg);
+      unsigned *const cost = static_cast<unsigned *>(arg_ptr(kCost));
+      if (cost) atomicAdd(&cost[tile], nseg);
+    }
+#if RTMI_TRACE
+    wsegs += nseg;
+    ++items_done;
+#endif
+    // flush: the item's sums (the lane index recomputed, not kept live)
+    int fl = int(threadIdx.x & 63u);
+    asm volatile("" : "+v"(fl));
+    if (fl < nv && !RTMI_RES_NOFLUSH) {
+      const int ly = fl / vw, lx = fl - ly * vw;
+      const size_t o3 = (size_t(y0 + ly) * size_t(arg(kW)) + size_t(x0 + lx)) * 3;
+#if RTMI_CHECK
+      if (o3 + 3 > a.out_elems) {
+        atomicAdd(&segments[5], 1ull);
+        atomicMax(&segments[6], (unsigned long long)o3);
+      } else
+#endif
+      if (arg(kOwns)) {
+        float *const o = static_cast<float *>(arg_ptr(kOut));
+        for (int c = 0; c < 3; ++c) o[o3 + c] = from_fixed((long long)acc[64 * c + fl]);
+      } else {
+        unsigned long long *const g = static_cast<unsigned long long *>(arg_ptr(kAccum));
+        for (int c = 0; c < 3; ++c) atomicAdd(&g[o3 + c], acc[64 * c + fl]);
+      }
+    }
+    for (int c = 0; c < 3; ++c) acc[64 * c + fl] = 0;
+#if RTMI_RES_TEAM
+    (void)next;
+    item = team_item();
+#else
+    item = arg(kFirst) + __builtin_amdgcn_readfirstlane(int(next));
+#endif
+  }
+  flush_counters(cnt, lane, segments);
+  RTMI_TRACE_END(items_done, wsegs)
 }
 
 // ---------------------------------------------------------------------------
@@ -900,6 +1199,11 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
 #ifndef RTMI_QUEUE_SLOTS
 #define RTMI_QUEUE_SLOTS 512
 #endif
+// waves per SIMD the queue kernel is compiled for: 8 (2 blocks per CU, 64
+// VGPRs) or 4 (one block per CU, 128 VGPRs and the whole LDS)
+#ifndef RTMI_QUEUE_PER_EU
+#define RTMI_QUEUE_PER_EU 8
+#endif
 constexpr int kQWaves = 16;
 constexpr int kQBins = RTMI_QUEUE_BINS;
 constexpr int kQSlots = RTMI_QUEUE_SLOTS;
@@ -949,7 +1253,7 @@ __device__ __forceinline__ int q_rank(unsigned long long m) {
 }
 
 template <int TW, bool FLAT>
-__global__ __launch_bounds__(64 * kQWaves, 8) void render_queue(
+__global__ __launch_bounds__(64 * kQWaves, RTMI_QUEUE_PER_EU) void render_queue(
     const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1, RenderArgs a,
     unsigned long long *__restrict__ accum, float *__restrict__ out, unsigned long long *__restrict__ segments,
     unsigned *__restrict__ counter) {
@@ -1463,6 +1767,8 @@ struct rt_ctx {
   int32_t cu_count = 0;                    // compute units of the device
   int32_t queue_blocks = 0;                // resident render_queue blocks for queue_lds dynamic LDS bytes
   size_t queue_lds = 0;
+  int32_t res_blocks = 0;                  // resident render_resident blocks for res_lds dynamic LDS bytes
+  size_t res_lds = 0;
   // BVH, built by rt_ctx_set_scene
   int32_t accel = RT_ACCEL_GRID;  // the fastest structure (brute force when the scene has none)
   SpherePair *big_pairs = nullptr;
@@ -1492,7 +1798,7 @@ struct rt_ctx {
   int32_t ordering = RT_ORDER_COST;
   // block-level accumulator flush of the automatic grid schedule (same image;
   // RTMI_BLOCK_FLUSH=0 in the environment turns it off, for A/B and tests)
-  bool block_flush = !(std::getenv("RTMI_BLOCK_FLUSH") && std::getenv("RTMI_BLOCK_FLUSH")[0] == '0');
+  bool block_flush = !RTMI_CHUNK_MAJOR && !(std::getenv("RTMI_BLOCK_FLUSH") && std::getenv("RTMI_BLOCK_FLUSH")[0] == '0');
   // a block that covers all samples of its tile writes the floats itself
   // (RTMI_BLOCK_OWNS=0 routes it through the accumulator, for A/B and tests)
   bool block_owns = !(std::getenv("RTMI_BLOCK_OWNS") && std::getenv("RTMI_BLOCK_OWNS")[0] == '0');
@@ -2057,7 +2363,8 @@ RTMI_EXPORT int rt_ctx_set_overlap(rt_ctx *ctx, int32_t overlapped) {
 
 RTMI_EXPORT int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind) {
   if (!ctx) return set_error(RT_EINVAL, "null ctx");
-  if (kind != RT_KERNEL_GRID && kind != RT_KERNEL_PERSISTENT && kind != RT_KERNEL_AUTO && kind != RT_KERNEL_QUEUE)
+  if (kind != RT_KERNEL_GRID && kind != RT_KERNEL_PERSISTENT && kind != RT_KERNEL_AUTO && kind != RT_KERNEL_QUEUE &&
+      kind != RT_KERNEL_RESIDENT)
     return set_error(RT_EINVAL, "unknown kernel kind");
   ctx->kernel = kind;
   return RT_OK;
@@ -2154,6 +2461,43 @@ int queue_resident_blocks(rt_ctx *ctx, size_t dyn) {
   return ctx->queue_blocks;
 }
 
+// resident blocks of render_resident with dyn bytes of dynamic LDS
+int res_resident_blocks(rt_ctx *ctx, size_t dyn) {
+  if (ctx->res_blocks <= 0 || ctx->res_lds != dyn) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_resident<8, 3>, 64 * kResWaves,
+                                                     dyn) != hipSuccess)
+      per_cu = 0;
+    ctx->res_blocks = std::max(1, per_cu) * std::max(1, ctx->cu_count);
+    ctx->res_lds = dyn;
+  }
+  return ctx->res_blocks;
+}
+
+// dynamic LDS of render_resident: the structure, then one sum set per wave
+// (RTMI_RES_LDS_PAD: analysis only, extra bytes per block)
+size_t res_lds_bytes(const Accel &acc, int kind, int32_t *acc_off) {
+  *acc_off = int32_t((accel_lds_bytes(acc, kind) + 15) / 16 * 16);
+  static const size_t pad = std::getenv("RTMI_RES_LDS_PAD") ? size_t(std::atol(std::getenv("RTMI_RES_LDS_PAD"))) : 0;
+  return size_t(*acc_off) + size_t(kResWaves) * 3 * 64 * 8 + pad;
+}
+
+template <int TW>
+void launch_resident(int acc, dim3 grid, size_t lds, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a,
+                     unsigned long long *accum, float *out) {
+#define RTMI_GO(K)                                                                                            \
+  hipLaunchKernelGGL((render_resident<TW, K>), grid, dim3(64 * kResWaves), lds, st, ctx->geom, ctx->sh0, ctx->sh1, a, \
+                     accum, out, ctx->segments, ctx->counter)
+  switch (acc) {
+    case 1: RTMI_GO(1); break;
+    case 2: RTMI_GO(2); break;
+    case 3: RTMI_GO(3); break;
+    case 4: RTMI_GO(4); break;
+    default: RTMI_GO(5); break;
+  }
+#undef RTMI_GO
+}
+
 template <int TW>
 void launch_queue(int acc, dim3 grid, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a,
                   unsigned long long *accum, float *out) {
@@ -2238,6 +2582,8 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   // the queue kernel: grid scenes, when selected
   const bool queue = (acc_kind == 2 || acc_kind == 3) && ctx->kernel == RT_KERNEL_QUEUE && TW <= 16;
   const int64_t qblocks = queue ? queue_resident_blocks(ctx, accel_lds_bytes(accel_of(ctx, acc_kind), acc_kind)) : 0;
+  // the resident grid kernel: accelerated scenes, when selected
+  const bool resident = bvh && !queue && ctx->kernel == RT_KERNEL_RESIDENT && TW <= 16;
   // the persistent kernel runs brute-force scenes only (see the note above stage_camera)
   const bool persistent = !bvh && (ctx->kernel == RT_KERNEL_PERSISTENT ||
                                    (ctx->kernel == RT_KERNEL_AUTO && tile_samples < 6000000));
@@ -2276,7 +2622,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   const int32_t spp1 = spp - tail;
   const int64_t grid_wpb = bvh ? GridShape<true>::waves : GridShape<false>::waves;
   int32_t nch1 = spp1 > 0 ? (spp1 + chunk1 - 1) / chunk1 : 0;
-  if (ctx->chunk <= 0 && !persistent && !queue && spp1 >= grid_wpb) {
+  if (ctx->chunk <= 0 && !persistent && !queue && (!resident || RTMI_RES_TEAM) && spp1 >= grid_wpb) {
     // automatic grid schedule: exactly a multiple of the block's waves items
     // per tile, so a block's items share a tile and it flushes once
     // (block_flush).  chunk1 = ceil(spp1 / n1) can leave the last items of a
@@ -2289,7 +2635,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   }
   chunk2 = std::min(chunk2, std::max(tail, 1));
   int32_t nch2 = tail > 0 ? (tail + chunk2 - 1) / chunk2 : 0;
-  if (ctx->tail_chunk <= 0 && !persistent && tail >= grid_wpb) {
+  if (ctx->tail_chunk <= 0 && !persistent && !resident && tail >= grid_wpb) {
     // the short-item phase in a multiple of the block's waves items per tile
     // too, so its blocks also cover one tile each and flush once
     int64_t n2 = (nch2 + grid_wpb - 1) / grid_wpb * grid_wpb;
@@ -2308,14 +2654,14 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   a.tiles = int32_t(tiles); a.spp1 = spp1; a.chunk1 = chunk1; a.nch1 = nch1; a.chunk2 = chunk2; a.nch2 = nch2;
   // block flush: every block's items are of one tile — both phases hold a
   // multiple of the block's waves items per tile
-  a.block_flush = !persistent && !queue && nch1 % grid_wpb == 0 && nch2 % grid_wpb == 0 && ctx->block_flush;
+  a.block_flush = !persistent && !queue && !resident && nch1 % grid_wpb == 0 && nch2 % grid_wpb == 0 && ctx->block_flush;
   a.block_owns_tile = a.block_flush && !pass_accum && nch1 == grid_wpb && nch2 == 0 && ctx->block_owns;
   // the queue kernel: an item that covers all its tile's samples writes the floats
-  if (queue) a.block_owns_tile = !pass_accum && nch1 == 1 && nch2 == 0;
+  if (queue || resident) a.block_owns_tile = !pass_accum && nch1 == 1 && nch2 == 0 && ctx->block_owns;
   const bool chunked = pass_accum || nch1 + nch2 > 1;
   if (!ctx->probing) {
     const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush + a.block_owns_tile, persistent ? 0 : 1,
-                              queue ? 2 : (persistent ? 1 : 0), acc_kind == 3 ? 2 : (acc_kind == 5 ? 4 : acc_kind)};
+                              queue ? 2 : (resident ? 3 : (persistent ? 1 : 0)), acc_kind == 3 ? 2 : (acc_kind == 5 ? 4 : acc_kind)};
     std::copy(sched, sched + 8, ctx->last_sched);
   }
   a.s_base = s_base;
@@ -2400,7 +2746,19 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   if (chunked && !pass_accum && !a.block_owns_tile)
     HIP_TRY(hipMemsetAsync(ctx->accum, 0, n_valid_out * sizeof(unsigned long long), st));
   dim3 grid;
-  if (queue) {
+  if (resident) {
+    // CU-resident blocks; waves past the first grid's take items from the counter
+    HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
+    RenderArgs b = a;
+    const size_t lds = res_lds_bytes(a.acc, acc_kind, &b.acc_off);
+    int64_t rblocks = res_resident_blocks(ctx, lds);
+    if (const char *e = std::getenv("RTMI_RES_BLOCKS")) rblocks = std::max<int64_t>(1, std::atoll(e));  // analysis only
+    grid = dim3(unsigned(std::min<int64_t>((items + kResWaves - 1) / kResWaves, rblocks)));
+    switch (TW) {
+      case 8: launch_resident<8>(acc_kind, grid, lds, st, ctx, b, accum, strip); break;
+      default: launch_resident<16>(acc_kind, grid, lds, st, ctx, b, accum, strip); break;
+    }
+  } else if (queue) {
     // CU-resident blocks pulling work items from a global counter
     HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
     grid = dim3(unsigned(std::min<int64_t>(items, qblocks)));
@@ -2418,7 +2776,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     const int64_t wpb = bvh ? GridShape<true>::waves : GridShape<false>::waves;
     grid = dim3(unsigned((items + wpb - 1) / wpb));
   }
-  if (!queue) switch (TW) {
+  if (!queue && !resident) switch (TW) {
     case 8: launch_shape<8>(persistent, acc_kind, chunked, grid, st, ctx, a, accum, strip); break;
     case 16: launch_shape<16>(persistent, acc_kind, chunked, grid, st, ctx, a, accum, strip); break;
     case 32: launch_shape<32>(persistent, acc_kind, chunked, grid, st, ctx, a, accum, strip); break;

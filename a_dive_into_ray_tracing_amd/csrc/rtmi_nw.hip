@@ -425,6 +425,30 @@ __global__ void finalize_kernel(const unsigned long long *__restrict__ acc, floa
   if (i < n) out[i] = float((long long)acc[i]) * 0x1p-32f;
 }
 
+// Closest hit of n given rays through the walk the renders use (validation:
+// rt_nw_debug_hits): the uniform grid staged in LDS as the grid kernels stage
+// it (GRID), or the BVH from global memory.  rays: {o.xyz, d.xyz, time, -} per
+// ray; keys: the segments' medium keys (null: 0).
+template <bool GRID>
+__global__ __launch_bounds__(256) void debug_hits_kernel(View sc, const float *__restrict__ rays,
+                                                         const unsigned long long *__restrict__ keys, int32_t n,
+                                                         int32_t *__restrict__ out_id, float *__restrict__ out_t,
+                                                         int32_t *__restrict__ out_face) {
+  stage_scene<false, false, GRID>(sc);  // (GRID: ends with the block barrier, before any thread leaves)
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float *r = rays + 8 * size_t(i);
+  const V o = mk(r[0], r[1], r[2]), d = mk(r[3], r[4], r[5]);
+  NwCount cnt{0, 0, 0, 0};
+  float t;
+  int face;
+  const int32_t k = GRID ? hit_world_nw_grid<false>(sc, o, d, r[6], keys ? keys[i] : 0ull, t, face, &cnt)
+                         : hit_world_nw<false, false>(sc, o, d, r[6], keys ? keys[i] : 0ull, t, face, &cnt);
+  out_id[i] = k < 0 ? -1 : k < sc.nobj ? sc.obj_id[k] : sc.med_id[k - sc.nobj];
+  out_t[i] = t;
+  out_face[i] = face;
+}
+
 }  // namespace nw
 }  // namespace rtmi
 
@@ -963,6 +987,49 @@ RTMI_EXPORT int rt_nw_debug_trace(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32
   (void)hipFree(d_rec);
   (void)hipFree(d_n);
   if (e != hipSuccess) return set_error(RT_EHIP, "rt_nw_debug_trace: %s", hipGetErrorString(e));
+  return RT_OK;
+}
+
+RTMI_EXPORT int rt_nw_debug_hits(rt_nw_ctx *ctx, const float *rays, const uint64_t *keys, int32_t n, int32_t *out_id,
+                                 float *out_t, int32_t *out_face) {
+  if (!ctx || (n > 0 && (!rays || !out_id || !out_t || !out_face)) || n < 0)
+    return set_error(RT_EINVAL, "rt_nw_debug_hits: bad argument");
+  if (ctx->nobj + ctx->nmed <= 0) return set_error(RT_EINVAL, "no scene uploaded (rt_nw_ctx_set_scene)");
+  if (n == 0) return RT_OK;
+  Guard g(ctx->device);
+  const bool grid = accel_used(ctx) == RT_NW_ACCEL_GRID;
+  const size_t lds = grid ? grid_bytes(ctx) : 0;
+  if (lds > kCuLds) return set_error(RT_EUNSUPPORTED, "rt_nw_debug_hits: grid of %zu B exceeds a CU's LDS", lds);
+  float *d_rays = nullptr, *d_t = nullptr;
+  unsigned long long *d_keys = nullptr;
+  int32_t *d_id = nullptr, *d_face = nullptr;
+  hipError_t e = hipMalloc(&d_rays, size_t(n) * 8 * sizeof(float));
+  if (e == hipSuccess && keys) e = hipMalloc(&d_keys, size_t(n) * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc(&d_t, size_t(n) * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&d_id, size_t(n) * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&d_face, size_t(n) * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMemcpy(d_rays, rays, size_t(n) * 8 * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess && keys) e = hipMemcpy(d_keys, keys, size_t(n) * sizeof(unsigned long long), hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    const dim3 grd(unsigned((n + 255) / 256)), blk(256);
+    if (grid)
+      hipLaunchKernelGGL(debug_hits_kernel<true>, grd, blk, lds, ctx->stream, view_of(ctx), d_rays, d_keys, n, d_id,
+                         d_t, d_face);
+    else
+      hipLaunchKernelGGL(debug_hits_kernel<false>, grd, blk, 0, ctx->stream, view_of(ctx), d_rays, d_keys, n, d_id,
+                         d_t, d_face);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) e = hipMemcpy(out_id, d_id, size_t(n) * sizeof(int32_t), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(out_t, d_t, size_t(n) * sizeof(float), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(out_face, d_face, size_t(n) * sizeof(int32_t), hipMemcpyDeviceToHost);
+  (void)hipFree(d_rays);
+  (void)hipFree(d_keys);
+  (void)hipFree(d_t);
+  (void)hipFree(d_id);
+  (void)hipFree(d_face);
+  if (e != hipSuccess) return set_error(RT_EHIP, "rt_nw_debug_hits: %s", hipGetErrorString(e));
   return RT_OK;
 }
 

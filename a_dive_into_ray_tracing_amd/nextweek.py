@@ -250,6 +250,20 @@ class NwRenderer:
         out = rec[: 12 * n.value].reshape(-1, 12).copy()
         return out[:, [0, 1, 2, 3, 4, 5, 6, 8, 9, 10]], out[:, [7, 11]].view(np.int32)
 
+    def debug_hits(self, rays, keys=None):
+        """Closest hit of each ray (rows o.xyz, d.xyz, time) through the walk
+        this context renders with: (insertion index or -1, t, box face)."""
+        n = len(rays)
+        r = np.zeros((n, 8), np.float32)
+        r[:, :7] = rays
+        k = None if keys is None else np.ascontiguousarray(keys, np.uint64)
+        idx, t, face = np.zeros(n, np.int32), np.zeros(n, np.float32), np.zeros(n, np.int32)
+        check(load().rt_nw_debug_hits(self._h, r.ctypes.data_as(_fp),
+                                      None if k is None else k.ctypes.data_as(C.POINTER(C.c_uint64)), n,
+                                      idx.ctypes.data_as(_ip), t.ctypes.data_as(_fp), face.ctypes.data_as(_ip)),
+              "rt_nw_debug_hits")
+        return idx, t, face
+
     def last_segments(self):
         v = C.c_uint64()
         check(load().rt_nw_ctx_last_segments(self._h, C.byref(v)), "rt_nw_ctx_last_segments")

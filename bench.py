@@ -262,6 +262,9 @@ def hw_queue_streams(torch, dev, n):
 
     def destroy():
         torch.cuda.synchronize(dev)
+        # torch's current stream is one of these (an ExternalStream): point it
+        # back at the default stream before the handles are freed
+        torch.cuda.set_stream(torch.cuda.default_stream(dev))
         for x in raw:
             hip.hipStreamDestroy(C.c_void_p(x))
 
@@ -356,6 +359,43 @@ def executed_flop(c, accel="bvh"):
     if accel == "grid":
         return c["segments"] * FLOP_PER_NODE_TEST + c["node_visits"] * FLOP_PER_CELL_STEP + spheres
     return c["node_visits"] * FLOP_PER_NODE_TEST + spheres
+
+
+# ------------------------------------------------ committed PMC records ----
+def timed_kernel_symbol(sched, flat):
+    """Mangled-name fragment of the render kernel a launch ran, from its
+    schedule (Renderer.last_schedule) and whether the grid is one y layer."""
+    if not sched:
+        return None
+    tw, kind, acc = sched["tile_w"], sched["persistent"], sched["bvh"]
+    a = {2: 3 if flat else 2, 4: 5 if flat else 4}.get(acc, acc)  # (last_schedule folds the one-layer kinds)
+    if kind == 3:
+        return f"render_residentILi{tw}ELi{a}E"
+    if kind == 0:
+        chunked = int(sched["items_per_tile"] + sched["tail_items_per_tile"] > 1)
+        return f"render_kernelILi{tw}ELb{chunked}ELi{a}E"
+    return None  # (persistent / queue: no committed record)
+
+
+def pmc_guard(record, lib_path, symbol):
+    """(record, None) when a committed PMC record (profiles/pmc_*.json) was
+    measured on the very kernel code this run timed — its "symbol" is the
+    timed kernel and its "code_sha1" the sha1 of that kernel's gfx950 code in
+    the loaded library — else (None, why).  A rebuilt kernel, another kernel
+    shape or a record without a hash is never quoted."""
+    from a_dive_into_ray_tracing_amd import codeobj
+
+    if not record or "code_sha1" not in record or "symbol" not in record:
+        return None, "record carries no kernel code hash"
+    if symbol != record["symbol"]:
+        return None, f"record measured on {record['symbol']}, this run timed {symbol}"
+    try:
+        _, h = codeobj.kernel_sha1(lib_path, symbol)
+    except Exception as e:  # (an unreadable library: not quoted)
+        return None, f"kernel code not readable: {e}"
+    if h != record["code_sha1"]:
+        return None, f"kernel code changed since the record (sha1 {h} vs {record['code_sha1']})"
+    return record, None
 
 
 # ------------------------------------------------------------ CPU baseline ----
@@ -554,7 +594,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--tail-spp", type=int, default=-1)
     ap.add_argument("--tail-chunk", type=int, default=0)
-    ap.add_argument("--kernel", choices=["auto", "persistent", "grid", "queue"], default="auto")
+    ap.add_argument("--kernel", choices=["auto", "persistent", "grid", "queue", "resident"], default="auto")
     ap.add_argument("--accel", choices=["none", "bvh", "grid"], default="grid",
                     help="closest-hit search: grid (default: uniform grid + DDA), bvh or brute force; same image bit for bit")
     ap.add_argument("--ordering", choices=["cost", "none"], default="cost")
@@ -729,6 +769,10 @@ def main():
     kernel_ms = busy_ms_per_launch(ev)
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     segs = r.last_segments()  # this rank's strip, last render
+    timed_sched = None if STUB else r.last_schedule()  # the timed launches' kernel (roofline.pmc guard)
+    # The side launches below run one at a time on context 0: the
+    # single-launch schedule, not the overlap hint of the timed steps
+    r.set_overlap(False)
     dist_info = None
     if N > 1:
         # the gather's own time (outside the timed region, where it overlaps
@@ -789,13 +833,35 @@ def main():
     one_shot = None
     if args.ordering == "cost" and not args.timed_only:
         r.set_ordering("cost")  # forgets the previous render's cost map
-        e0, e1 = timed_render()
+        if N > 1:
+            # One render as the reference's use case does it, on every rank: from
+            # a common start (barrier) to the end of the blocking gather of the
+            # strips at rank 0, max over ranks
+            collective("barrier before the one-shot render", dist.barrier)
+            sync()
+            t1 = time.perf_counter()
+            e0, e1 = timed_render()
+            collective("one-shot gather", rdist.gather_strips, strip if coll.type == dev.type else strip.cpu(), rank, N,
+                       dst=0)
+            sync()
+            os_wall = time.perf_counter() - t1
+            t = torch.tensor([os_wall], dtype=torch.float64, device=coll)
+            collective("all_reduce(max) of the one-shot render", dist.all_reduce, t, op=dist.ReduceOp.MAX)
+            os_wall = float(t.item())
+        else:
+            e0, e1 = timed_render()
         r.set_ordering("none")
         e2, e3 = timed_render()
         sync()
         one_shot = {"probe_ordered_ms": round(e0.elapsed_time(e1), 3), "image_order_ms": round(e2.elapsed_time(e3), 3)}
         if N == 1:  # this rank's rows are the whole workload (or the --strip-of strip)
             one_shot["msamples_per_s"] = round(nrows_valid * W * SPP / (one_shot["probe_ordered_ms"] * 1e-3) / 1e6, 3)
+        else:  # the whole frame over N GPUs: render with its probe + gather, wall clock, max over ranks
+            one_shot["wall_ms_max_rank"] = round(os_wall * 1e3, 3)
+            one_shot["msamples_per_s"] = round(W * H * SPP / os_wall / 1e6, 3)
+            one_shot["note"] = ("one render of the frame from a common barrier to the end of the blocking gather at "
+                                "rank 0 (cost probe included), host wall clock, max over ranks; probe_ordered_ms is "
+                                "rank 0's render alone (HIP events)")
         r.set_ordering(args.ordering)
 
     # The brute-force kernel's own VALU roofline: one more launch of the same
@@ -828,13 +894,16 @@ def main():
                 flop_exec = None
         achieved = flop_exec / (kernel_ms * 1e-3) / 1e12 if flop_exec else None
         eq_ach = flop_eq / (kernel_ms * 1e-3) / 1e12
-        traffic = None
+        traffic, pmc_notes = None, {}
+        lib_path = None if STUB else rt._abi.LIB_PATH
+        ksym = None if STUB else timed_kernel_symbol(timed_sched, r.grid_info()[0][1] == 1)
         pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc) and args.workload == "config2" and not args.strip_of and N == 1:  # measured on config 2
+        if os.path.exists(pmc) and args.workload == "config2" and not args.strip_of and N == 1 and not STUB:  # measured on config 2
             try:
-                traffic = (json.load(open(pmc)).get(args.accel) or {}).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+                rec, pmc_notes["traffic"] = pmc_guard(json.load(open(pmc)).get(args.accel), lib_path, ksym)
+                traffic = rec["hbm_bytes_per_launch"] if rec else None
+            except Exception as e:
+                traffic, pmc_notes["traffic"] = None, f"unreadable: {e}"
         roof = {
             "bound": "valu",
             "achieved": round(achieved, 3) if achieved else None,
@@ -886,11 +955,16 @@ def main():
         # included) and how busy the VALU issue is — the bound of this
         # divergent kernel
         pmcv = os.path.join(REPO, "profiles", "pmc_valu.json")
-        if os.path.exists(pmcv) and args.workload == "config2" and args.accel == "grid" and not args.strip_of and N == 1:
+        if (os.path.exists(pmcv) and args.workload == "config2" and args.accel == "grid" and not args.strip_of and N == 1
+                and not STUB):
             try:
-                pv = json.load(open(pmcv))
+                pv, pmc_notes["pmc"] = pmc_guard(json.load(open(pmcv)), lib_path, ksym)
+                roof["pmc"] = None
+            except Exception as e:
+                pv, pmc_notes["pmc"] = None, f"unreadable: {e}"
+            try:
                 ks = kernel_ms * 1e-3
-                roof["pmc"] = {
+                roof["pmc"] = None if pv is None else {
                     "source": "profiles/pmc_valu.json",
                     "executed_fp32_flop_per_launch": pv["executed_fp32_flop_per_launch"],
                     "executed_fp32_frac": round(pv["executed_fp32_flop_per_launch"] / ks / 1e12 / PEAK_FP32_TFLOPS, 4),
@@ -900,6 +974,9 @@ def main():
                 }
             except Exception:
                 pass
+        pmc_notes = {k: v for k, v in pmc_notes.items() if v}
+        if pmc_notes:  # why roofline.traffic / roofline.pmc are null
+            roof["pmc_guard"] = {"timed_kernel": ksym, **pmc_notes}
         if why:
             roof["note"] = why
         line = {
@@ -950,12 +1027,12 @@ def main():
             line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)
         if gather_check is not None and not gather_check["bit_exact_vs_1gpu_frame"]:
-            close_all(rs, destroy_streams)
             dist.destroy_process_group()
+            close_all(rs, destroy_streams)
             sys.exit(3)
-    close_all(rs, destroy_streams)
-    if N > 1:
+    if N > 1:  # (before the streams its collectives ran on are destroyed)
         dist.destroy_process_group()
+    close_all(rs, destroy_streams)
 
 
 def close_all(rs, destroy_streams):

@@ -149,8 +149,11 @@ int rt_ctx_set_overlap(rt_ctx *ctx, int32_t overlapped);
  * otherwise.  RT_KERNEL_QUEUE: CU-resident 16-wave blocks that share an LDS
  * pool of rays binned by the length of their next grid walk (grid scenes,
  * tiles of 8 or 16 columns; otherwise as RT_KERNEL_AUTO).
- * All give bit-identical images. */
-enum { RT_KERNEL_GRID = 0, RT_KERNEL_PERSISTENT = 1, RT_KERNEL_AUTO = 2, RT_KERNEL_QUEUE = 3 };
+ * RT_KERNEL_RESIDENT: CU-resident 16-wave blocks whose waves each run the grid
+ * kernel's loop over work items taken from a global counter (accelerated
+ * scenes, tiles of 8 or 16 columns; otherwise as RT_KERNEL_AUTO; DESIGN.md
+ * §4.7).  All give bit-identical images. */
+enum { RT_KERNEL_GRID = 0, RT_KERNEL_PERSISTENT = 1, RT_KERNEL_AUTO = 2, RT_KERNEL_QUEUE = 3, RT_KERNEL_RESIDENT = 4 };
 int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind);
 
 /* Closest-hit search.  RT_ACCEL_NONE: brute force over all spheres, the

@@ -173,6 +173,13 @@ int rt_nw_render_rows(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32_t W, int32_
  * xyz and the box face (int32 bits, -1: none).  *n = segments. */
 int rt_nw_debug_trace(rt_nw_ctx *ctx, const rt_nw_camera *cam, int32_t W, int32_t H, int32_t max_depth,
                       uint64_t seed, int32_t i, int32_t j, int32_t s, float *rec, int32_t cap, int32_t *n);
+/* Validation: the closest hit of n given rays through the walk a render of
+ * this context uses (the uniform grid or the BVH: rt_nw_ctx_accel_info) —
+ * rays {o.xyz, d.xyz, time, unused} per ray (8 floats), keys the segments'
+ * medium keys (null: 0).  Out: the winner's insertion index (-1: miss), t
+ * and the box face (-1: none), as one segment of rt_nw_debug_trace. */
+int rt_nw_debug_hits(rt_nw_ctx *ctx, const float *rays, const uint64_t *keys, int32_t n, int32_t *out_id, float *out_t,
+                     int32_t *out_face);
 /* world.hit calls of the last render (waits for it). */
 int rt_nw_ctx_last_segments(rt_nw_ctx *ctx, uint64_t *segments);
 /* Diagnostic: the kernel of the last render, {persistent, uniform grid,

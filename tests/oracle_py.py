@@ -280,6 +280,23 @@ def nw_trace(flat, nwcam, W, H, depth, seed, i, j, smp, cap=64):
     return out[:, [0, 1, 2, 3, 4, 5, 6, 8, 9, 10]], out[:, [7, 11]].view(np.int32)
 
 
+def nw_hits(flat, rays, keys=None):
+    """Oracle mirror of NwRenderer.debug_hits: the brute-force closest hit of
+    each ray (rows o.xyz, d.xyz, time): (insertion index or -1, t, box face)."""
+    L = _nw_bind()
+    L.or_nw_hits.argtypes = [C.POINTER(OrNwScene), _fp, C.POINTER(C.c_uint64), C.c_int32, _ip, _fp, _ip]
+    L.or_nw_hits.restype = None
+    s = nw_scene(flat)
+    n = len(rays)
+    r = np.zeros((n, 8), np.float32)
+    r[:, :7] = rays
+    k = None if keys is None else np.ascontiguousarray(keys, np.uint64)
+    idx, t, face = np.zeros(n, np.int32), np.zeros(n, np.float32), np.zeros(n, np.int32)
+    L.or_nw_hits(C.byref(s), r.ctypes.data_as(_fp), None if k is None else k.ctypes.data_as(C.POINTER(C.c_uint64)), n,
+                 idx.ctypes.data_as(_ip), t.ctypes.data_as(_fp), face.ctypes.data_as(_ip))
+    return idx, t, face
+
+
 def row_mean_z(frame_rows, S, a, b, s_ab):
     """Per-row, per-channel z-scores of a frame's row means against two
     independent oracle renders of the same rows (sums at s_ab spp under two

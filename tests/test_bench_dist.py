@@ -17,7 +17,7 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("n,pipeline", [(2, 2), (3, 2), (2, 1)])
+@pytest.mark.parametrize("n,pipeline", [(2, 2), (3, 2), (2, 1), (8, 2)])
 def test_bench_n_ranks_line_schema(n, pipeline, tmp_path):
     """pipeline 2 (the default): the steps alternate over two render contexts
     and two strip buffers; 3 timed steps reuse a buffer after its gather."""
@@ -50,6 +50,12 @@ def test_bench_n_ranks_line_schema(n, pipeline, tmp_path):
     assert gc["rows"] == 800 and gc["bit_exact_vs_1gpu_frame"] is True and gc["max_abs_diff"] == 0.0
     assert "cpu_baseline" not in d  # rank 0 at N = 1 only
     assert d["roofline"]["kernel_ms_max_rank"] == max(di["kernel_ms_per_rank"])
+    # the single-render figure beside the pipelined value —
+    # one render of the whole frame plus its blocking gather, max over ranks
+    os_ = d["one_shot"]
+    assert os_["wall_ms_max_rank"] > 0 and "max over ranks" in os_["note"]
+    assert d["one_shot_msamples_per_s"] == os_["msamples_per_s"]
+    assert abs(os_["msamples_per_s"] - 1200 * 800 * 500 / (os_["wall_ms_max_rank"] * 1e-3) / 1e6) <= 1e-3 * os_["msamples_per_s"] + 1e-3
 
 
 def test_stub_requires_gloo():

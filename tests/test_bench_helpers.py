@@ -2,6 +2,7 @@
 FLOP count over the flattened scenes, and the strip partition it uses."""
 import os
 import sys
+import pytest
 
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -106,3 +107,47 @@ def test_busy_ms_per_launch_unions_overlapping_launches():
     assert bench.busy_ms_per_launch(pairs([(0, 10), (10, 20), (20, 30)])) == 10
     assert bench.busy_ms_per_launch(pairs([(0, 20), (1, 21), (20, 40), (21, 41)])) == 41 / 4
     assert bench.busy_ms_per_launch(pairs([(5, 6), (0, 2)])) == 1.5  # a gap is not counted; any order
+
+
+LIB = os.path.join(REPO, "a_dive_into_ray_tracing_amd", "lib", "librtmi.so")
+
+
+def test_timed_kernel_symbol_names_the_instantiation():
+    frame = {"tile_w": 8, "items_per_tile": 4, "tail_items_per_tile": 0, "persistent": 0, "bvh": 2}
+    assert bench.timed_kernel_symbol(frame, flat=True) == "render_kernelILi8ELb1ELi3E"
+    assert bench.timed_kernel_symbol(frame, flat=False) == "render_kernelILi8ELb1ELi2E"
+    assert bench.timed_kernel_symbol(dict(frame, items_per_tile=1), flat=True) == "render_kernelILi8ELb0ELi3E"
+    assert bench.timed_kernel_symbol(dict(frame, persistent=3, tile_w=16), flat=True) == "render_residentILi16ELi3E"
+    assert bench.timed_kernel_symbol(dict(frame, bvh=4), flat=True) == "render_kernelILi8ELb1ELi5E"
+    assert bench.timed_kernel_symbol(dict(frame, persistent=2), flat=True) is None
+    assert bench.timed_kernel_symbol(None, flat=True) is None
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="needs the built library")
+def test_pmc_records_are_quoted_only_for_the_kernel_they_measured():
+    """roofline.traffic / roofline.pmc come from committed
+    PMC records; bench.py quotes them only while the timed kernel's gfx950
+    code hashes as the record says, and reports why otherwise."""
+    import json
+
+    from a_dive_into_ray_tracing_amd import codeobj
+
+    sym = "render_kernelILi8ELb1ELi3E"
+    full, h = codeobj.kernel_sha1(LIB, sym)
+    assert full and sym in full and len(h) == 40
+    rec = {"symbol": sym, "code_sha1": h, "hbm_bytes_per_launch": 1}
+    assert bench.pmc_guard(rec, LIB, sym) == (rec, None)
+    # a perturbed hash (the kernel was rebuilt since the record): not quoted
+    got, why = bench.pmc_guard(dict(rec, code_sha1="0" * 40), LIB, sym)
+    assert got is None and "changed" in why
+    # another kernel timed: not quoted
+    got, why = bench.pmc_guard(rec, LIB, "render_residentILi8ELi3E")
+    assert got is None and "render_residentILi8ELi3E" in why
+    # no hash at all: not quoted
+    got, why = bench.pmc_guard({"hbm_bytes_per_launch": 1}, LIB, sym)
+    assert got is None and "no kernel code hash" in why
+    # the committed records name a kernel of this library by its current code
+    for path, key in (("pmc_valu.json", None), ("pmc_traffic.json", "grid")):
+        d = json.load(open(os.path.join(REPO, "profiles", path)))
+        d = d[key] if key else d
+        assert codeobj.kernel_sha1(LIB, d["symbol"])[1] is not None

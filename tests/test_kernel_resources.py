@@ -53,7 +53,7 @@ def kernel_metadata(tmp_path):
             if not m:
                 continue
             fields = dict(re.findall(r"\.(vgpr_count|private_segment_fixed_size|group_segment_fixed_size"
-                                     r"|vgpr_spill_count):\s+(\d+)", "." + block))
+                                     r"|vgpr_spill_count|sgpr_spill_count|sgpr_count):\s+(\d+)", "." + block))
             meta[m.group(1)] = {k: int(v) for k, v in fields.items()}
     return meta
 

@@ -13,7 +13,7 @@ for f in sorted(glob.glob(f"{root}/pmc*/*_counter_collection.csv")):
     names = {}
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if any(n in k for n in ("render_kernel", "render_persistent", "render_queue", "finalize_kernel")):
+        if any(n in k for n in ("render_kernel", "render_persistent", "render_queue", "render_resident", "finalize_kernel")):
             per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
             names[r["Dispatch_Id"]] = k.split("(")[0]
     for (dsp, c), v in per.items():

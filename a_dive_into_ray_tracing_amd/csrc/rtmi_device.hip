@@ -131,10 +131,13 @@ __device__ unsigned g_trace_n;
 #ifndef RTMI_SYNC_PROBE
 #define RTMI_SYNC_PROBE 0
 #endif
-// analysis only (A/B): work items numbered chunk-major, so a grid-kernel
-// block's waves render four different tiles (what tile locality is worth)
-#ifndef RTMI_CHUNK_MAJOR
-#define RTMI_CHUNK_MAJOR 0
+// The experimental build (make experimental -> lib/librtmi_experimental.so):
+// the two kernels measured slower than render_kernel — the queue kernel
+// (RT_KERNEL_QUEUE) and the resident grid kernel
+// (RT_KERNEL_RESIDENT, §4.7) — kept, tested, out of the product library,
+// where those kinds run the automatic choice.
+#ifndef RTMI_EXPERIMENTAL
+#define RTMI_EXPERIMENTAL 0
 #endif
 #ifndef RTMI_PAIR_GROUP
 #define RTMI_PAIR_GROUP 4
@@ -411,13 +414,8 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
 
   auto item_range = [&](int it, int &tl, int &sb, int &n) {
     if (it < a.tiles * a.nch1) {
-#if RTMI_CHUNK_MAJOR  // analysis only: a block's waves on different tiles (block_flush off)
-      tl = it % a.tiles;
-      sb = (it / a.tiles) * a.chunk1;
-#else
       tl = it / a.nch1;
       sb = (it - tl * a.nch1) * a.chunk1;
-#endif
       n = max(0, min(a.chunk1, a.spp1 - sb));  // 0: an empty item of the automatic schedule
     } else {
       const int i2 = it - a.tiles * a.nch1;
@@ -645,8 +643,10 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   }
 }
 
+#if RTMI_EXPERIMENTAL
 // ---------------------------------------------------------------------------
-// resident grid kernel (RT_KERNEL_RESIDENT)
+// resident grid kernel (RT_KERNEL_RESIDENT; experimental
+// build only: measured 3% slower than render_kernel, profiles/r06/resident/)
 // ---------------------------------------------------------------------------
 // render_kernel's per-wave loop in CU-resident blocks: each wave takes work
 // items from a global counter until none is left, with its own fixed-point
@@ -664,22 +664,6 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
 #define RTMI_RES_WAVES 16
 #endif
 constexpr int kResWaves = RTMI_RES_WAVES;
-// analysis variants (A/B only, never the product): RTMI_RES_NOFLUSH=1 skips
-// the flush's global writes (wrong image: what the flush costs),
-// RTMI_RES_STATIC=1 assigns items round-robin instead of by the counter
-#ifndef RTMI_RES_NOFLUSH
-#define RTMI_RES_NOFLUSH 0
-#endif
-#ifndef RTMI_RES_STATIC
-#define RTMI_RES_STATIC 0
-#endif
-// RTMI_RES_TEAM=1 (analysis): waves 4t..4t+3 of a block (one per SIMD) take
-// the four items of one tile together, as a grid-kernel block does — the
-// team's first wave at round r claims the tile group, the others read it
-// from an LDS ring (no overflow protection: A/B only)
-#ifndef RTMI_RES_TEAM
-#define RTMI_RES_TEAM 0
-#endif
 static_assert(kResWaves >= 1 && kResWaves <= 16, "a block holds at most 16 waves");
 
 template <int TW, int ACC>
@@ -751,36 +735,7 @@ __global__ __launch_bounds__(64 * kResWaves, 8) void render_resident(
   };
   // the first item by position, the next ones from the counter (which the
   // host zeroes: items past the grid's first gridDim.x * kResWaves)
-#if RTMI_RES_TEAM
-  __shared__ uint32_t team_round[kResWaves / 4];
-  __shared__ unsigned long long team_ring[kResWaves / 4][64];
-  if (threadIdx.x < kResWaves / 4) team_round[threadIdx.x] = 0;
-  if (threadIdx.x < kResWaves / 4 * 64) (&team_ring[0][0])[threadIdx.x] = ~0ull;
-  __syncthreads();
-  uint32_t round = 0;
-  auto team_item = [&]() {
-    const int t = wave >> 2;
-    unsigned long long v = 0;
-    if (lane == 0) {
-      if (atomicCAS(&team_round[t], round, round + 1) == round) {
-        const unsigned g = atomicAdd(static_cast<unsigned *>(arg_ptr(kCounter)), 1u);
-        v = (uint64_t(round) << 32) | g;
-        __hip_atomic_store(&team_ring[t][round & 63], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else {
-        for (;;) {
-          v = __hip_atomic_load(&team_ring[t][round & 63], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (uint32_t(v >> 32) == round) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-    }
-    ++round;
-    return 4 * __builtin_amdgcn_readfirstlane(int(uint32_t(v))) + (wave & 3);
-  };
-  int item = team_item();
-#else
   int item = blockIdx.x * kResWaves + wave;
-#endif
   while (item < arg(kNItems)) {
     int tile, s0, ns;
     {
@@ -887,13 +842,7 @@ __global__ __launch_bounds__(64 * kResWaves, 8) void render_resident(
     // the next item's claim first: its latency overlaps the flush
     unsigned next = 0;
     if (lane == 0) {
-#if RTMI_RES_STATIC
-      next = unsigned(item);
-#elif RTMI_RES_TEAM
-      next = 0;
-#else
       next = atomicAdd(static_cast<unsigned *>(arg_ptr(kCounter)), 1u);
-#endif
       atomicAdd(static_cast<unsigned long long *>(arg_ptr(kSegs)), (unsigned long long)nseg);
       unsigned *const cost = static_cast<unsigned *>(arg_ptr(kCost));
       if (cost) atomicAdd(&cost[tile], nseg);
@@ -905,7 +854,7 @@ __global__ __launch_bounds__(64 * kResWaves, 8) void render_resident(
     // flush: the item's sums (the lane index recomputed, not kept live)
     int fl = int(threadIdx.x & 63u);
     asm volatile("" : "+v"(fl));
-    if (fl < nv && !RTMI_RES_NOFLUSH) {
+    if (fl < nv) {
       const int ly = fl / vw, lx = fl - ly * vw;
       const size_t o3 = (size_t(y0 + ly) * size_t(arg(kW)) + size_t(x0 + lx)) * 3;
 #if RTMI_CHECK
@@ -923,16 +872,12 @@ __global__ __launch_bounds__(64 * kResWaves, 8) void render_resident(
       }
     }
     for (int c = 0; c < 3; ++c) acc[64 * c + fl] = 0;
-#if RTMI_RES_TEAM
-    (void)next;
-    item = team_item();
-#else
     item = arg(kFirst) + __builtin_amdgcn_readfirstlane(int(next));
-#endif
   }
   flush_counters(cnt, lane, segments);
   RTMI_TRACE_END(items_done, wsegs)
 }
+#endif  // RTMI_EXPERIMENTAL
 
 // ---------------------------------------------------------------------------
 // persistent render kernel: continuous per-wave job stream over work items
@@ -1168,6 +1113,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
   (void)n_taken;
 }
 
+#if RTMI_EXPERIMENTAL
 // ---------------------------------------------------------------------------
 // queue kernel: CU-resident 16-wave blocks sharing one LDS pool of rays,
 // binned by the pre-walk bound
@@ -1282,7 +1228,7 @@ __global__ __launch_bounds__(64 * kQWaves, RTMI_QUEUE_PER_EU) void render_queue(
   const SceneView<float> sc{geom, sh0, sh1, a.n};
   SegCounters cnt{};
   unsigned nseg = 0;
-  bool fault = false;  // a watchdog fired (segments[7]): leave
+  bool fault = false;  // a watchdog fired (segments[7] bit 63, sticky in segments[8]): leave
 
   // the lane's ray: o, d, T, generator, meta = depth (bits 0-23) | pixel in
   // the tile (24-29) | item slot (30-31); its big-sphere result (t_max, best:
@@ -1504,7 +1450,9 @@ __global__ __launch_bounds__(64 * kQWaves, RTMI_QUEUE_PER_EU) void render_queue(
     if (lane == 0) q_store(reinterpret_cast<uint32_t *>(&Q.item[s][7]), 0u);
   };
 
-  uint32_t idle = 0;
+  // (counter[1] != 0: the idle watchdog fires at the first pass — fault
+  // injection for tests, RTMI_QUEUE_FAULT_INJECT)
+  uint32_t idle = counter[1] != 0u ? kQIdleMax + 1u : 0u, seen_progress = 0;
 #if RTMI_STATS
   unsigned npass = 0;
 #endif
@@ -1566,9 +1514,24 @@ __global__ __launch_bounds__(64 * kQWaves, RTMI_QUEUE_PER_EU) void render_queue(
     }
     QPH(1)
     const unsigned long long live = __ballot(has);
-    if (live == 0) ++idle;
+    if (live == 0) {
+      // idle passes count only while the block makes no progress: a wave
+      // waiting for a free item slot behind long paths is not stuck
+      // (ADVICE r05); progress = paths ended, all item slots
+      uint32_t prog = 0;
+      for (int k = 0; k < kQItems; ++k) prog += q_load(&Q.done[k]);
+      prog = q_uniform(prog);
+      if (prog != seen_progress) {
+        seen_progress = prog;
+        idle = 0;
+      }
+      ++idle;
+    }
     if (__ballot(fault) || idle > kQIdleMax) {
-      if (lane == 0) atomicOr(&segments[7], 1ull << 63);  // watchdog: rt_render / rt_ctx_synchronize report RT_EHIP
+      if (lane == 0) {  // watchdog: reported as RT_EHIP by every call that waits for the render (check_queue_fault)
+        atomicOr(&segments[7], 1ull << 63);
+        atomicOr(&segments[8], 1ull);  // sticky: not cleared by the next pass's counters
+      }
       break;
     }
     if (live == 0) {
@@ -1629,6 +1592,7 @@ __global__ __launch_bounds__(64 * kQWaves, RTMI_QUEUE_PER_EU) void render_queue(
 #endif
   flush_counters(cnt, lane, segments);
 }
+#endif  // RTMI_EXPERIMENTAL (queue kernel)
 
 // Closest hit of n given rays by the brute-force loop and by the BVH
 // (validation: rt_ctx_debug_hits).  rays = {o.xyz, d.xyz} per ray.
@@ -1768,6 +1732,7 @@ struct rt_ctx {
   int32_t queue_blocks = 0;                // resident render_queue blocks for queue_lds dynamic LDS bytes
   size_t queue_lds = 0;
   int32_t res_blocks = 0;                  // resident render_resident blocks for res_lds dynamic LDS bytes
+  bool queue_launched = false;             // a queue kernel ran on this context (check_queue_fault)
   size_t res_lds = 0;
   // BVH, built by rt_ctx_set_scene
   int32_t accel = RT_ACCEL_GRID;  // the fastest structure (brute force when the scene has none)
@@ -1798,7 +1763,7 @@ struct rt_ctx {
   int32_t ordering = RT_ORDER_COST;
   // block-level accumulator flush of the automatic grid schedule (same image;
   // RTMI_BLOCK_FLUSH=0 in the environment turns it off, for A/B and tests)
-  bool block_flush = !RTMI_CHUNK_MAJOR && !(std::getenv("RTMI_BLOCK_FLUSH") && std::getenv("RTMI_BLOCK_FLUSH")[0] == '0');
+  bool block_flush = !(std::getenv("RTMI_BLOCK_FLUSH") && std::getenv("RTMI_BLOCK_FLUSH")[0] == '0');
   // a block that covers all samples of its tile writes the floats itself
   // (RTMI_BLOCK_OWNS=0 routes it through the accumulator, for A/B and tests)
   bool block_owns = !(std::getenv("RTMI_BLOCK_OWNS") && std::getenv("RTMI_BLOCK_OWNS")[0] == '0');
@@ -1838,8 +1803,14 @@ struct rt_ctx {
   bool overlap = false;
 };
 
+namespace {
+int check_queue_fault(rt_ctx *ctx, hipStream_t st);
+}  // namespace
 namespace rtmi {
 hipStream_t ctx_stream(rt_ctx *ctx) { return ctx->stream; }
+// RT_EHIP when a queue kernel's watchdog fired on this context since its last
+// whole render or accumulator reset (rt_multi's gather checks every device)
+int ctx_fault(rt_ctx *ctx) { return check_queue_fault(ctx, ctx->stream); }
 }  // namespace rtmi
 
 namespace {
@@ -1914,9 +1885,10 @@ RTMI_EXPORT int rt_ctx_create(int32_t device, rt_ctx **out) {
   ctx->device = device;
   HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&ctx->last_done, hipEventDisableTiming));
-  if (int rc = dev_alloc(&ctx->segments, 8)) return rc;
-  HIP_TRY(hipMemset(ctx->segments, 0, 8 * sizeof(unsigned long long)));
-  if (int rc = dev_alloc(&ctx->counter, 1)) return rc;
+  // [0..7] the last render's counters, [8] the queue kernel's sticky watchdog flag
+  if (int rc = dev_alloc(&ctx->segments, 9)) return rc;
+  HIP_TRY(hipMemset(ctx->segments, 0, 9 * sizeof(unsigned long long)));
+  if (int rc = dev_alloc(&ctx->counter, 2)) return rc;  // work-item counter; [1] fault injection (queue kernel)
   {
     // resident blocks per CU for the persistent grid; over-subscription is
     // harmless (extra waves start later and find the counter exhausted)
@@ -2448,6 +2420,7 @@ void launch_tw(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const
                        ctx->sh0, ctx->sh1, ctx->pairs, b, accum, out, ctx->segments);
 }
 
+#if RTMI_EXPERIMENTAL
 // resident blocks of the queue kernel with dyn bytes of dynamic LDS (the grid)
 int queue_resident_blocks(rt_ctx *ctx, size_t dyn) {
   if (ctx->queue_blocks <= 0 || ctx->queue_lds != dyn) {
@@ -2475,11 +2448,9 @@ int res_resident_blocks(rt_ctx *ctx, size_t dyn) {
 }
 
 // dynamic LDS of render_resident: the structure, then one sum set per wave
-// (RTMI_RES_LDS_PAD: analysis only, extra bytes per block)
 size_t res_lds_bytes(const Accel &acc, int kind, int32_t *acc_off) {
   *acc_off = int32_t((accel_lds_bytes(acc, kind) + 15) / 16 * 16);
-  static const size_t pad = std::getenv("RTMI_RES_LDS_PAD") ? size_t(std::atol(std::getenv("RTMI_RES_LDS_PAD"))) : 0;
-  return size_t(*acc_off) + size_t(kResWaves) * 3 * 64 * 8 + pad;
+  return size_t(*acc_off) + size_t(kResWaves) * 3 * 64 * 8;
 }
 
 template <int TW>
@@ -2509,6 +2480,7 @@ void launch_queue(int acc, dim3 grid, hipStream_t st, const rt_ctx *ctx, const R
     hipLaunchKernelGGL((render_queue<TW, false>), grid, dim3(64 * kQWaves), lds, st, ctx->geom, ctx->sh0, ctx->sh1, a,
                        accum, out, ctx->segments, ctx->counter);
 }
+#endif  // RTMI_EXPERIMENTAL
 
 template <int TW>
 void launch_shape(bool persistent, int acc, bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx,
@@ -2541,7 +2513,9 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     hipStream_t s;
     ~MarkDone() { (void)hipEventRecord(c->last_done, s); }
   } mark_done{ctx, st};
-  HIP_TRY(hipMemsetAsync(ctx->segments, 0, 8 * sizeof(unsigned long long), st));
+  // (a progressive pass keeps [8], the queue kernel's sticky fault flag, for
+  // rt_accum_resolve; a whole render starts without one)
+  HIP_TRY(hipMemsetAsync(ctx->segments, 0, (pass_accum ? 8 : 9) * sizeof(unsigned long long), st));
   if (nrows == 0) return RT_OK;
   // valid rows: row0 + r*row_step < H
   int32_t nvalid = 0;
@@ -2580,10 +2554,16 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
                            : (ctx->accel != RT_ACCEL_NONE && ctx->nnodes > 0 ? 1 : 0);
   const bool bvh = acc_kind != 0;
   // the queue kernel: grid scenes, when selected
-  const bool queue = (acc_kind == 2 || acc_kind == 3) && ctx->kernel == RT_KERNEL_QUEUE && TW <= 16;
+  // (the product build runs the automatic choice for both: they measured
+  // slower than the grid kernel; RTMI_EXPERIMENTAL builds only)
+  const bool queue = RTMI_EXPERIMENTAL && (acc_kind == 2 || acc_kind == 3) && ctx->kernel == RT_KERNEL_QUEUE && TW <= 16;
+#if RTMI_EXPERIMENTAL
   const int64_t qblocks = queue ? queue_resident_blocks(ctx, accel_lds_bytes(accel_of(ctx, acc_kind), acc_kind)) : 0;
+#else
+  const int64_t qblocks = 0;
+#endif
   // the resident grid kernel: accelerated scenes, when selected
-  const bool resident = bvh && !queue && ctx->kernel == RT_KERNEL_RESIDENT && TW <= 16;
+  const bool resident = RTMI_EXPERIMENTAL && bvh && !queue && ctx->kernel == RT_KERNEL_RESIDENT && TW <= 16;
   // the persistent kernel runs brute-force scenes only (see the note above stage_camera)
   const bool persistent = !bvh && (ctx->kernel == RT_KERNEL_PERSISTENT ||
                                    (ctx->kernel == RT_KERNEL_AUTO && tile_samples < 6000000));
@@ -2622,7 +2602,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   const int32_t spp1 = spp - tail;
   const int64_t grid_wpb = bvh ? GridShape<true>::waves : GridShape<false>::waves;
   int32_t nch1 = spp1 > 0 ? (spp1 + chunk1 - 1) / chunk1 : 0;
-  if (ctx->chunk <= 0 && !persistent && !queue && (!resident || RTMI_RES_TEAM) && spp1 >= grid_wpb) {
+  if (ctx->chunk <= 0 && !persistent && !queue && !resident && spp1 >= grid_wpb) {
     // automatic grid schedule: exactly a multiple of the block's waves items
     // per tile, so a block's items share a tile and it flushes once
     // (block_flush).  chunk1 = ceil(spp1 / n1) can leave the last items of a
@@ -2747,25 +2727,31 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     HIP_TRY(hipMemsetAsync(ctx->accum, 0, n_valid_out * sizeof(unsigned long long), st));
   dim3 grid;
   if (resident) {
+#if RTMI_EXPERIMENTAL
     // CU-resident blocks; waves past the first grid's take items from the counter
     HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
     RenderArgs b = a;
     const size_t lds = res_lds_bytes(a.acc, acc_kind, &b.acc_off);
-    int64_t rblocks = res_resident_blocks(ctx, lds);
-    if (const char *e = std::getenv("RTMI_RES_BLOCKS")) rblocks = std::max<int64_t>(1, std::atoll(e));  // analysis only
+    const int64_t rblocks = res_resident_blocks(ctx, lds);
     grid = dim3(unsigned(std::min<int64_t>((items + kResWaves - 1) / kResWaves, rblocks)));
     switch (TW) {
       case 8: launch_resident<8>(acc_kind, grid, lds, st, ctx, b, accum, strip); break;
       default: launch_resident<16>(acc_kind, grid, lds, st, ctx, b, accum, strip); break;
     }
+#endif
   } else if (queue) {
+#if RTMI_EXPERIMENTAL
     // CU-resident blocks pulling work items from a global counter
-    HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
+    HIP_TRY(hipMemsetAsync(ctx->counter, 0, 2 * sizeof(unsigned), st));
+    const char *inject = std::getenv("RTMI_QUEUE_FAULT_INJECT");  // (read per launch: tests toggle it)
+    if (inject && inject[0] == '1') HIP_TRY(hipMemsetAsync(ctx->counter + 1, 1, 1, st));  // tests: the watchdog path
+    ctx->queue_launched = true;
     grid = dim3(unsigned(std::min<int64_t>(items, qblocks)));
     switch (TW) {
       case 8: launch_queue<8>(acc_kind, grid, st, ctx, a, accum, strip); break;
       default: launch_queue<16>(acc_kind, grid, st, ctx, a, accum, strip); break;
     }
+#endif
   } else if (persistent) {
     // a resident grid of waves pulling items from a global counter
     HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
@@ -2826,6 +2812,7 @@ RTMI_EXPORT int rt_accum_reset(rt_ctx *ctx, int32_t W, int32_t nrows) {
   ctx->pass_spp = 0;
   if (ctx->last_stream) HIP_TRY(hipStreamSynchronize(ctx->last_stream));  // no pass still adding
   if (n) HIP_TRY(hipMemsetAsync(ctx->pass_accum, 0, n * sizeof(unsigned long long), ctx->stream));
+  HIP_TRY(hipMemsetAsync(ctx->segments + 8, 0, sizeof(unsigned long long), ctx->stream));  // (queue kernel's fault flag)
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return RT_OK;
 }
@@ -2874,7 +2861,8 @@ RTMI_EXPORT int rt_accum_resolve(rt_ctx *ctx, float *dev_sum, float *host_sum, v
     if (n) HIP_TRY(hipMemcpyAsync(host_sum, out, n * sizeof(float), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
   }
-  return RT_OK;
+  // a pass whose queue kernel's watchdog fired left samples out
+  return check_queue_fault(ctx, st);
 }
 
 // Checkpoint / resume: the raw fixed-point accumulator (W*nrows*3 int64) and
@@ -2986,11 +2974,11 @@ namespace {
 // idle loop that waited far past any legitimate delay) marks segments[7]
 // bit 63 and the kernel leaves early — the image is then incomplete.
 int check_queue_fault(rt_ctx *ctx, hipStream_t st) {
-  if (ctx->last_sched[6] != 2) return RT_OK;
+  if (!ctx->queue_launched) return RT_OK;
   unsigned long long v = 0;
-  HIP_TRY(hipMemcpyAsync(&v, ctx->segments + 7, sizeof v, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&v, ctx->segments + 8, sizeof v, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  if (v >> 63) return set_error(RT_EHIP, "queue kernel watchdog fired: the render is incomplete");
+  if (v) return set_error(RT_EHIP, "queue kernel watchdog fired: the render is incomplete");
   return RT_OK;
 }
 }  // namespace
@@ -3130,13 +3118,15 @@ RTMI_EXPORT int rt_ctx_debug_hits(rt_ctx *ctx, const float *rays, int32_t n, int
       (rc = dev_alloc(&d_t, size_t(n) * 2)))
     return rc;
   HIP_TRY(hipMemcpy(d_rays, rays, size_t(n) * 6 * sizeof(float), hipMemcpyHostToDevice));
-  // the walk the renders use (3: the one-layer grid walk)
-  const int kind = ctx->accel == RT_ACCEL_GRID
-                       ? (ctx->grid_ok && ctx->grid.n[1] == 1 ? 3 : 2) + (ctx->grid_ok && ctx->grid_global ? 2 : 0)
-                       : 1;
-  if ((kind == 1 && !ctx->nnodes) || (kind >= 2 && !ctx->grid_ok)) {
+  // the walk the renders use, by render_rows_impl's rule (3: the one-layer
+  // grid walk; +2: walked in global memory; 1: the BVH, also where the grid
+  // setting has no grid, e.g. over 65 535 spheres)
+  const int kind = ctx->accel == RT_ACCEL_GRID && ctx->grid_ok
+                       ? (ctx->grid.n[1] == 1 ? 3 : 2) + (ctx->grid_global ? 2 : 0)
+                       : (ctx->accel != RT_ACCEL_NONE && ctx->nnodes > 0 ? 1 : 0);
+  if (kind == 0) {
     (void)hipFree(d_rays); (void)hipFree(d_idx); (void)hipFree(d_t);
-    return set_error(RT_EUNSUPPORTED, "rt_ctx_debug_hits: no %s for this scene", kind >= 2 ? "grid" : "BVH");
+    return set_error(RT_EUNSUPPORTED, "rt_ctx_debug_hits: brute force only for this scene and setting (no structure)");
   }
   const Accel acc = accel_of(ctx, kind);
   const size_t lds = accel_lds_bytes(acc, kind);

@@ -1,5 +1,7 @@
 """The queue kernel (RT_KERNEL_QUEUE) against the oracle and
-the other kernels, bit for bit.
+the other kernels, bit for bit — on the experimental build
+(lib/librtmi_experimental.so: `make -C a_dive_into_ray_tracing_amd/csrc
+experimental`), run by tests/test_gpu_experimental.py in a child process.
 
 Rays migrate between the waves of a block through the LDS pool and end in
 whichever wave holds them; the per-pixel sums are integers, so every order
@@ -124,6 +126,35 @@ def test_queue_progressive_passes(world, queue_renderer):
     for s0, n in ((0, 5), (5, 1), (6, 6)):
         queue_renderer.render_pass(cam, W, H, s0, n)
     assert np.array_equal(queue_renderer.accum_resolve(), want)
+
+
+def test_queue_watchdog_fault_is_reported(world, queue_renderer, monkeypatch):
+    """a pass whose queue kernel's watchdog fired (injected here:
+    RTMI_QUEUE_FAULT_INJECT=1 trips the idle watchdog at the first pass) left
+    samples out; the fault is sticky until the next accumulator reset or
+    whole render, so a resolve after that pass — and after further clean
+    passes — fails with RT_EHIP, as does a render that faults itself.  A
+    reset clears it and the same passes then resolve to the oracle's image."""
+    W, H = 64, 40
+    cam = rt.final_camera(W / H)
+    queue_renderer.accum_reset(W, H)
+    monkeypatch.setenv("RTMI_QUEUE_FAULT_INJECT", "1")
+    queue_renderer.render_pass(cam, W, H, 0, 3)
+    monkeypatch.delenv("RTMI_QUEUE_FAULT_INJECT")
+    queue_renderer.render_pass(cam, W, H, 3, 3)
+    for _ in range(2):
+        with pytest.raises(rt.RTError, match="RT_EHIP"):
+            queue_renderer.accum_resolve()
+    queue_renderer.accum_reset(W, H)
+    for s0 in (0, 3):
+        queue_renderer.render_pass(cam, W, H, s0, 3)
+    assert np.array_equal(queue_renderer.accum_resolve(), O.fast_render(o_scene(world), o_cam(cam), W, H, 6, 50, SEED))
+    monkeypatch.setenv("RTMI_QUEUE_FAULT_INJECT", "1")
+    with pytest.raises(rt.RTError, match="RT_EHIP"):
+        queue_renderer.render(cam, W, H, 6, 50, SEED)
+    monkeypatch.delenv("RTMI_QUEUE_FAULT_INJECT")
+    assert np.array_equal(queue_renderer.render(cam, W, H, 6, 50, SEED),
+                          O.fast_render(o_scene(world), o_cam(cam), W, H, 6, 50, SEED))
 
 
 def test_queue_repeated_renders_are_identical(queue_renderer):

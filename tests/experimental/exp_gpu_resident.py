@@ -1,5 +1,7 @@
 """The resident grid kernel (RT_KERNEL_RESIDENT) against the
-oracle and the grid kernel, bit for bit.
+oracle and the grid kernel, bit for bit — on the experimental build
+(lib/librtmi_experimental.so), run by tests/test_gpu_experimental.py in a
+child process.
 
 Its waves take work items from a global counter, so which wave renders which
 item changes from run to run; the per-pixel sums are integers flushed per

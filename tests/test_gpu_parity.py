@@ -224,9 +224,27 @@ def test_large_scenes_bit_exact_vs_oracle(n):
             ran.add((accel, r.last_schedule()["bvh"]))
             assert np.array_equal(got, want), (accel, np.abs(got - want).max())
             assert r.last_segments() == want_segs, accel
+        # the validation entry point takes the walk these renders take (the
+        # global grid, or past 65 535 spheres the global BVH):
+        # 20 000 rays through the sphere layer, closest hit == brute force
+        r.set_accel("grid")
+        L = rt.load()
+        L.rt_ctx_debug_hits.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32),
+                                        C.POINTER(C.c_float)]
+        m = 20_000
+        o = np.column_stack([g.uniform(-45, 45, m), g.uniform(0.0, 3.0, m), g.uniform(-45, 45, m)])
+        dv = g.normal(size=(m, 3)) * [1.0, 0.2, 1.0]
+        rays = np.ascontiguousarray(np.column_stack([o, dv]).astype(np.float32))
+        idx, t = np.zeros(2 * m, np.int32), np.zeros(2 * m, np.float32)
+        rc = L.rt_ctx_debug_hits(r._h, rays.ctypes.data_as(C.POINTER(C.c_float)), m,
+                                 idx.ctypes.data_as(C.POINTER(C.c_int32)), t.ctypes.data_as(C.POINTER(C.c_float)))
     finally:
         r.close()
     assert ran == {("grid", 4 if n <= 65535 else 1), ("bvh", 1), ("none", 0)}, ran
+    assert rc == 0
+    idx, t = idx.reshape(m, 2), t.reshape(m, 2)
+    assert (idx[:, 0] >= 0).mean() > 0.5
+    assert np.array_equal(idx[:, 0], idx[:, 1]) and np.array_equal(t[:, 0], t[:, 1])
 
 
 def test_max_depth_limit(learn_renderer):

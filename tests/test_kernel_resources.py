@@ -72,3 +72,14 @@ def test_frame_kernel_register_budget(tmp_path):
         # static LDS (camera, block counters, grid descriptor): the 20 KB a block
         # may use at 8 blocks per CU minus the record slots and sums (§4.5)
         assert m["group_segment_fixed_size"] <= 256, (name[0], m)
+
+
+@pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(f"{LLVM}/llvm-readelf")),
+                    reason="needs the built library and ROCm's llvm tools")
+def test_product_library_holds_no_experimental_kernel(tmp_path):
+    """the kernels that measured slower than the grid
+    kernel (queue, resident) are not in librtmi.so, only in the experimental
+    build; the product's render kernels are all there."""
+    meta = kernel_metadata(tmp_path)
+    assert not [k for k in meta if "render_queue" in k or "render_resident" in k]
+    assert [k for k in meta if "render_kernelILi8ELb1ELi3E" in k]

@@ -1,9 +1,11 @@
 #!/bin/bash
-# Per-wave timelines (RTMI_TRACE build, lib/librtmi_trace.so — build it first:
-# make -C a_dive_into_ray_tracing_amd/csrc variant NAME=trace VFLAGS=-DRTMI_TRACE=1)
-# of the kernel shapes in KERNELS, whole frame and one rank's 1/8 strip.
+# Per-wave timelines (RTMI_TRACE build, lib/librtmi_wavetrace.so — build it on
+# the CPU first: python tools/variants.py build wavetrace) of the kernel shapes
+# in KERNELS, whole frame and one rank's 1/8 strip.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
+python tools/variants.py check wavetrace || exit 1
+export TRACE_LIB=librtmi_wavetrace.so
 OUT=gpurun_out/${TAG:-trace_ab}; mkdir -p $OUT
 for k in ${KERNELS:-grid resident}; do
   for s in 1 8; do

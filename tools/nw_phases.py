@@ -1,5 +1,6 @@
-"""Phase split of the Next-Week kernel (RTMI_NW_PHASES build, run on the GPU box):
-make -C a_dive_into_ray_tracing_amd/csrc nwvariant NAME=nwph VFLAGS="-DRTMI_NW_PHASES=1"
+"""Phase split of the Next-Week kernel (RTMI_NW_PHASES build, run on the GPU box;
+built on the CPU first: python tools/variants.py build nwph — a build from
+other sources is refused)
 Prints, per scene and structure, the share of a wave's item time in the closest
 hit, in hit record + texture + scatter, and in accumulation + regeneration."""
 import ctypes as C
@@ -10,6 +11,11 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import variants  # noqa: E402
+
+if variants.check("nwph"):
+    sys.exit(variants.check("nwph"))
 os.environ["RTMI_LIBRARY"] = os.path.join(ROOT, "a_dive_into_ray_tracing_amd", "lib", "librtmi_nwph.so")
 import torch  # noqa: E402,F401  (one HIP runtime)
 import a_dive_into_ray_tracing_amd.nextweek as nw  # noqa: E402

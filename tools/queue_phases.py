@@ -1,6 +1,6 @@
 """Phase clocks of the queue kernel (analysis only): the RTMI_QUEUE_PHASES
-build (lib/librtmi_qph.so: make -C a_dive_into_ray_tracing_amd/csrc variant
-NAME=qph VFLAGS=-DRTMI_QUEUE_PHASES=1) renders config 2 (or argv W H S) once
+build (lib/librtmi_qph.so, built on the CPU first: python tools/variants.py
+build qph; a build from other sources is refused) renders config 2 (or argv W H S) once
 through the queue kernel and prints each phase's share of the waves' cycles:
 generation, exchange, idle passes, segment (walk + shading), end of segment
 (accumulation, next big-sphere pass and key, flushes)."""
@@ -9,7 +9,14 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ.setdefault("RTMI_LIBRARY", os.path.join(REPO, "a_dive_into_ray_tracing_amd", "lib", "librtmi_qph.so"))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+import variants  # noqa: E402
+
+if "RTMI_LIBRARY" not in os.environ:
+    why = variants.check("qph")
+    if why:
+        sys.exit(why)
+    os.environ["RTMI_LIBRARY"] = os.path.join(REPO, "a_dive_into_ray_tracing_amd", "lib", "librtmi_qph.so")
 sys.path.insert(0, REPO)
 import a_dive_into_ray_tracing_amd as rt  # noqa: E402
 

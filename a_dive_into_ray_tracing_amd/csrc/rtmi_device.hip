@@ -535,7 +535,7 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
 #if RTMI_TRACE_PHASES
     const unsigned long long cyc_b = __builtin_amdgcn_s_memtime();
     cyc_iter += cyc_b - cyc_a;  // hit + shading of this pass (wave-level)
-    const bool ramp = pbase + 64 >= nq && ppos == 64;  // the item's jobs all taken: the wave's ramp-down
+    const bool ramp = pbase + ppos >= nq;  // the item's jobs all handed out: the wave's ramp-down
 #endif
     const unsigned long long m = __ballot(done);
     if (m) {

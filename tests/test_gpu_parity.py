@@ -243,7 +243,7 @@ def test_large_scenes_bit_exact_vs_oracle(n):
     assert ran == {("grid", 4 if n <= 65535 else 1), ("bvh", 1), ("none", 0)}, ran
     assert rc == 0
     idx, t = idx.reshape(m, 2), t.reshape(m, 2)
-    assert (idx[:, 0] >= 0).mean() > 0.5
+    assert (idx[:, 0] >= 0).mean() > 0.2 and (idx[:, 0] > 0).mean() > 0.05  # (index 0: the ground)
     assert np.array_equal(idx[:, 0], idx[:, 1]) and np.array_equal(t[:, 0], t[:, 1])
 
 

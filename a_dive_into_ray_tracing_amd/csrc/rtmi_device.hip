@@ -132,10 +132,11 @@ __device__ unsigned g_trace_n;
 #define RTMI_SYNC_PROBE 0
 #endif
 // The experimental build (make experimental -> lib/librtmi_experimental.so):
-// the two kernels measured slower than render_kernel — the queue kernel
-// (RT_KERNEL_QUEUE) and the resident grid kernel
-// (RT_KERNEL_RESIDENT, §4.7) — kept, tested, out of the product library,
-// where those kinds run the automatic choice.
+// the resident grid kernel (RT_KERNEL_RESIDENT), measured
+// slower than render_kernel — kept and tested, out of the product library,
+// where RT_KERNEL_RESIDENT runs the automatic choice.  (The queue kernel of
+// round 5, RT_KERNEL_QUEUE, was retired in round 6: 33-44% slower and a ring
+// stall in ~2% of renders; git show 1b6ce15:a_dive_into_ray_tracing_amd/csrc/rtmi_device.hip)
 #ifndef RTMI_EXPERIMENTAL
 #define RTMI_EXPERIMENTAL 0
 #endif
@@ -195,7 +196,7 @@ template <bool BVH> struct GridShape {
 // grid it measured slower than the grid kernel everywhere (round 2: config 2
 // frame / 1/8 strip 30.9 / 4.72 ms against 26.0 / 3.70; profiles/README.md),
 // so RT_KERNEL_PERSISTENT with an accelerator runs the grid kernel.  (The
-// CU-resident design of round 5, render_queue, is RT_KERNEL_QUEUE.)
+// CU-resident designs of rounds 5-6 are DESIGN.md §4.6-4.7.)
 
 // The camera and the reciprocals of main.cpp:278-279's (W-1, H-1)
 // denominators in LDS (21 floats), read at each regeneration instead of held
@@ -284,14 +285,11 @@ constexpr bool acc_gmem(int A) { return A >= 4; }
 // absorption, or the scattered ray with its robustness offset.  Returns true
 // when the path ended: col is then its colour (black when absorbed or out of
 // depth).  Shared by every fast kernel, so they compute identical paths.
-// FROM_BIG (the queue kernel): the grid's big-sphere pass was run when the
-// ray was made; its result (t_max0, best0) starts the walk.
-template <int ACC, bool FROM_BIG = false>
+template <int ACC>
 __device__ __forceinline__ bool path_segment(const SceneView<float> &sc, const SpherePair *__restrict__ pairs,
                                              const RenderArgs &a, V3<float> &o, V3<float> &d, V3<float> &T,
                                              int &depth, Xoro &rng, V3<float> &col, SegCounters &cnt,
-                                             unsigned long long *segments, float t_max0 = INFINITY,
-                                             int32_t best0 = -1) {
+                                             unsigned long long *segments) {
   (void)cnt, (void)segments;
   float t;
 #if RTMI_TRACE
@@ -306,14 +304,14 @@ __device__ __forceinline__ bool path_segment(const SceneView<float> &sc, const S
 #endif
     );
   } else if constexpr (ACC >= 2) {
-    k = hit_world_grid<kBigGroup, acc_flat(ACC), FROM_BIG, acc_gmem(ACC)>(a.acc, o, d, t, key
+    k = hit_world_grid<kBigGroup, acc_flat(ACC), acc_gmem(ACC)>(a.acc, o, d, t, key
 #if RTMI_STATS
                                    , cnt.bvh_stats
 #endif
 #if RTMI_TRACE_PHASES
                                    , cnt.pc
 #endif
-                                   , t_max0, best0);
+                                   );
   } else {
     k = hit_world_packed<kPairGroup>(pairs, a.npairs, o, d, t
 #if RTMI_STATS
@@ -1113,486 +1111,6 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, RTMI_PERSIST_MIN_BLOCKS) void 
   (void)n_taken;
 }
 
-#if RTMI_EXPERIMENTAL
-// ---------------------------------------------------------------------------
-// queue kernel: CU-resident 16-wave blocks sharing one LDS pool of rays,
-// binned by the pre-walk bound
-// ---------------------------------------------------------------------------
-// The grid kernel's waves each walk their own 64 paths: a wave pays for its
-// longest walk, so the walk runs at 0.34 lane utilisation.  Here a block's
-// waves share a pool of kQSlots waiting rays in LDS, kept in kQBins bins by
-// the bound on their next walk's cell count (grid_bound, from the big-sphere
-// pass run when the ray is made).  Each pass a wave picks the fullest bin:
-// lanes whose ray is in it keep it, the others swap theirs for one of that
-// bin's rays, so the wave walks rays of similar length together
-// (tools/grid_sim.c: cell-step lane utilisation 0.35 -> 0.82 with 8 bins of a
-// 512-ray pool).  No wave waits for another: bins are multi-producer /
-// multi-consumer rings of slot indices in LDS (a claim by compare-and-swap on
-// the ring head, a push by atomic add on its tail, entries polled until
-// written), so the only coupling is the pool.  All of it lives in LDS, so the
-// fences order LDS only (s_waitcnt lgkmcnt(0), no wait on global memory).  Camera jobs come from block
-// work items (tile, sample range) held in kQItems LDS slots with their
-// fixed-point sums: a ray carries its item slot and pixel, whichever wave ends
-// the path adds its colour there, and the wave that ends an item's last path
-// writes the item out.  Integer sums: the image is bit-identical to every
-// other kernel's, in any order of rays and waves.
-#ifndef RTMI_QUEUE_BINS
-#define RTMI_QUEUE_BINS 8
-#endif
-#ifndef RTMI_QUEUE_PHASES
-#define RTMI_QUEUE_PHASES 0
-#endif
-#ifndef RTMI_QUEUE_SLOTS
-#define RTMI_QUEUE_SLOTS 512
-#endif
-// waves per SIMD the queue kernel is compiled for: 8 (2 blocks per CU, 64
-// VGPRs) or 4 (one block per CU, 128 VGPRs and the whole LDS)
-#ifndef RTMI_QUEUE_PER_EU
-#define RTMI_QUEUE_PER_EU 8
-#endif
-constexpr int kQWaves = 16;
-constexpr int kQBins = RTMI_QUEUE_BINS;
-constexpr int kQSlots = RTMI_QUEUE_SLOTS;
-constexpr int kQFree = kQBins;  // the ring of free slots
-constexpr int kQRings = kQBins + 1;
-constexpr int kQItems = 4;  // item slots per block (2 bits of a ray's meta word)
-constexpr uint32_t kQEmpty = 0xFFFFFFFFu;
-constexpr uint32_t kQSpinMax = 1u << 20;  // watchdog: polls of one ring entry
-constexpr uint32_t kQIdleMax = 1u << 20;  // watchdog: passes without a live lane
-// the jobs word: item slot (bits 29-31) | camera jobs handed out (bits 0-28)
-constexpr uint32_t kQJobBits = 29, kQJobMask = (1u << kQJobBits) - 1u;
-constexpr uint32_t kQNone = 4u, kQSwitching = 5u, kQDrained = 6u;  // slot field: no item yet / being replaced / no items left
-static_assert((kQSlots & (kQSlots - 1)) == 0 && kQSlots <= 32768, "ring positions wrap by mask; slot indices are 16-bit");
-// A ring entry is (lap << 16 | slot index), lap = position / kQSlots mod 2^16:
-// a slow consumer of position t must not take the value a pusher of t +
-// kQSlots wrote there first (its pushers and consumers can be a lap apart
-// once other waves recycle slots), so a consumer waits for its own lap's tag
-// and a pusher writes only into an empty entry, by compare-and-swap.
-static_assert(kQBins >= 2 && kQBins <= 32, "bins");
-
-struct QueueLds {
-  float4 ray[4][kQSlots];         // o|T.x, d|T.y, T.z|t_max|meta|best, xoroshiro state
-  uint32_t ring[kQRings][kQSlots];  // lap << 16 | slot index (kQEmpty: not yet written / consumed)
-  uint32_t head[kQRings], tail[kQRings];
-  unsigned long long acc[kQItems][3][64];  // fixed-point sums per item slot
-  int32_t item[kQItems][8];        // x0, y0, vw, nv, s_base + s0, tile, nq, live
-  uint32_t done[kQItems], segs[kQItems];  // paths ended; their segments (the tile's cost)
-  uint32_t jobs;
-};
-
-__device__ __forceinline__ uint32_t q_load(const uint32_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void q_store(uint32_t *p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ uint32_t q_add(uint32_t *p, uint32_t v) {
-  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ bool q_cas(uint32_t *p, uint32_t expected, uint32_t desired) {
-  return __hip_atomic_compare_exchange_strong(p, &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ uint32_t q_uniform(uint32_t v) { return uint32_t(__builtin_amdgcn_readfirstlane(int(v))); }
-__device__ __forceinline__ int q_rank(unsigned long long m) {
-  return __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
-}
-
-template <int TW, bool FLAT>
-__global__ __launch_bounds__(64 * kQWaves, RTMI_QUEUE_PER_EU) void render_queue(
-    const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1, RenderArgs a,
-    unsigned long long *__restrict__ accum, float *__restrict__ out, unsigned long long *__restrict__ segments,
-    unsigned *__restrict__ counter) {
-  constexpr int ACC = FLAT ? 3 : 2;
-  __shared__ QueueLds Q;
-  __shared__ float cam_lds[21];
-  const int lane = threadIdx.x & 63;
-  for (int i = threadIdx.x; i < kQRings * kQSlots; i += blockDim.x) {
-    const int r = i / kQSlots, k = i - r * kQSlots;
-    Q.ring[r][k] = r == kQFree ? uint32_t(k) : kQEmpty;  // the free ring: lap 0, every slot
-  }
-  for (int i = threadIdx.x; i < kQItems * 3 * 64; i += blockDim.x) (&Q.acc[0][0][0])[i] = 0;
-  if (threadIdx.x < kQRings) {
-    Q.head[threadIdx.x] = 0;
-    Q.tail[threadIdx.x] = threadIdx.x == kQFree ? kQSlots : 0;
-  }
-  if (threadIdx.x < kQItems) {
-    Q.item[threadIdx.x][7] = 0;
-    Q.done[threadIdx.x] = 0;
-    Q.segs[threadIdx.x] = 0;
-  }
-  if (threadIdx.x == 0) Q.jobs = kQNone << kQJobBits;
-  stage_camera(cam_lds, a);
-  stage_grid(a.acc);  // (ends with the block barrier: the only one)
-
-  const SceneView<float> sc{geom, sh0, sh1, a.n};
-  SegCounters cnt{};
-  unsigned nseg = 0;
-  bool fault = false;  // a watchdog fired (segments[7] bit 63, sticky in segments[8]): leave
-
-  // the lane's ray: o, d, T, generator, meta = depth (bits 0-23) | pixel in
-  // the tile (24-29) | item slot (30-31); its big-sphere result (t_max, best:
-  // record-slot key) and bin key
-  V3<float> o = mk(0.f, 0.f, 0.f), d = o, T = o;
-  Xoro rng{0, 0};
-  int meta = 0, best = -1, key = 0;
-  float tmax = 0.f;
-  bool has = false;
-
-  // ---- ring operations --------------------------------------------------
-  // Claim up to `want` entries of ring r (wave-level; head and tail are read
-  // again after a failed compare-and-swap).  Returns the count, h the first.
-  auto claim = [&](int r, int want, uint32_t &h) {
-    uint32_t hh = 0, nn = 0;
-    if (lane == 0) {
-      for (int tries = 0; tries < 256; ++tries) {
-        hh = q_load(&Q.head[r]);
-        const uint32_t tt = q_load(&Q.tail[r]);
-        const int avail = int(tt - hh);
-        nn = uint32_t(max(0, min(want, avail)));
-        if (nn == 0 || q_cas(&Q.head[r], hh, hh + nn)) break;
-        nn = 0;
-      }
-    }
-    h = q_uniform(hh);
-    return int(q_uniform(nn));
-  };
-  // The slot index at position pos of ring r, for the lanes with `want`:
-  // polled until the entry carries this position's lap, then marked consumed.
-  auto take = [&](int r, uint32_t pos, bool want) {
-    volatile uint32_t *e = &Q.ring[r][pos & (kQSlots - 1)];
-    const uint32_t lap = (pos / uint32_t(kQSlots)) & 0xFFFFu;
-    uint32_t v = 0;
-    bool pend = want;
-    for (uint32_t spin = 0; __ballot(pend); ++spin) {
-      if (pend) {
-        const uint32_t x = *e;
-        if ((x >> 16) == lap) {
-          *e = kQEmpty;
-          v = x & 0xFFFFu;
-          pend = false;
-        }
-      }
-      if (spin > kQSpinMax) {
-        fault = true;
-        pend = false;
-      }
-      if (__ballot(pend)) __builtin_amdgcn_s_sleep(1);
-    }
-    return v;
-  };
-  // Push slot s onto ring r (per lane; lanes with `want`): a tail position,
-  // polled until its previous entry has been consumed, then written.
-  auto put = [&](int r, uint32_t s, bool want) {
-    uint32_t pos = 0;
-    if (want) pos = q_add(&Q.tail[r], 1u);
-    uint32_t *e = &Q.ring[want ? r : 0][pos & (kQSlots - 1)];
-    const uint32_t val = (((pos / uint32_t(kQSlots)) & 0xFFFFu) << 16) | s;
-    bool pend = want;
-    for (uint32_t spin = 0; __ballot(pend); ++spin) {
-      if (pend && q_cas(e, kQEmpty, val)) pend = false;
-      if (spin > kQSpinMax) {
-        fault = true;
-        pend = false;
-      }
-      if (__ballot(pend)) __builtin_amdgcn_s_sleep(1);
-    }
-  };
-  auto store_ray = [&](uint32_t s) {
-    Q.ray[0][s] = make_float4(o.x, o.y, o.z, T.x);
-    Q.ray[1][s] = make_float4(d.x, d.y, d.z, T.y);
-    Q.ray[2][s] = make_float4(T.z, tmax, __int_as_float(meta), __int_as_float(best));
-    Q.ray[3][s] = make_float4(__uint_as_float(uint32_t(rng.s0)), __uint_as_float(uint32_t(rng.s0 >> 32)),
-                              __uint_as_float(uint32_t(rng.s1)), __uint_as_float(uint32_t(rng.s1 >> 32)));
-  };
-
-  // ---- camera jobs ------------------------------------------------------
-  bool drained = false;  // wave-uniform: no block work item left
-  // Claim up to `want` camera jobs of the block's current item (moving the
-  // block to its next item once this one is handed out).  Returns the count
-  // n (0: none now), with the item slot and the first job.  Wave-uniform.
-  auto claim_jobs = [&](int want, int &slot, int &j0) {
-    for (int attempt = 0; attempt < 8; ++attempt) {
-      const uint32_t v = q_uniform(q_load(&Q.jobs));
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");  // the item fields after the word naming them
-      const uint32_t s = v >> kQJobBits;
-      if (s == kQDrained) {
-        drained = true;
-        return 0;
-      }
-      if (s == kQSwitching) return 0;  // another wave is fetching the next item
-      if (s < kQItems && int(v & kQJobMask) < Q.item[s][6]) {
-        uint32_t old = 0;
-        if (lane == 0) old = q_add(&Q.jobs, uint32_t(want));
-        old = q_uniform(old);
-        const uint32_t s2 = old >> kQJobBits;
-        if (s2 >= kQItems) continue;  // the word changed state meanwhile (this add is overwritten)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-        const int jj = int(old & kQJobMask), nq = Q.item[s2][6];
-        if (jj >= nq) continue;
-        slot = int(s2);
-        j0 = jj;
-        return min(want, nq - jj);
-      }
-      // handed out (or no item yet): fetch the next item into a free slot
-      uint32_t won = 0;
-      if (lane == 0) won = q_cas(&Q.jobs, v, kQSwitching << kQJobBits) ? 1u : 0u;
-      if (!q_uniform(won)) continue;
-      int f = -1;
-      for (int k = 0; k < kQItems && f < 0; ++k)
-        if (q_uniform(q_load(reinterpret_cast<uint32_t *>(&Q.item[k][7]))) == 0) f = k;
-      if (f < 0) {  // every slot still has paths in flight: retry later
-        if (lane == 0) q_store(&Q.jobs, v);
-        return 0;
-      }
-      for (;;) {
-        unsigned itn = 0;
-        if (lane == 0) itn = atomicAdd(counter, 1u);
-        itn = q_uniform(itn);
-        if (int(itn) >= a.n_items) {
-          if (lane == 0) q_store(&Q.jobs, kQDrained << kQJobBits);
-          drained = true;
-          return 0;
-        }
-        const ItemDesc cd = describe_item<TW>(a, int(itn));
-        if (cd.nq <= 0) continue;  // an empty item: nothing to render
-        if (lane < 8) {
-          const int fld[8] = {cd.x0, cd.y0, cd.vw, cd.nv, a.s_base + cd.s0, cd.tile, cd.nq, 1};
-          int x = fld[0];
-#pragma unroll
-          for (int k = 1; k < 8; ++k) x = lane == k ? fld[k] : x;
-          Q.item[f][lane] = x;
-        }
-        if (lane == 0) {
-          Q.done[f] = 0;
-          Q.segs[f] = 0;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        if (lane == 0) q_store(&Q.jobs, uint32_t(f) << kQJobBits);
-        break;
-      }
-    }
-    return 0;
-  };
-
-  // Camera rays straight into the pool: all 64 lanes make one each (with its
-  // big-sphere pass and bin key) and park it in a free slot, so a lane holds
-  // one ray at a time and generation runs with every lane busy.
-  auto generate = [&]() {
-    uint32_t hf = 0;
-    const int nf = claim(kQFree, 64, hf);
-    if (nf == 0) return;
-    int slot = 0, j0 = 0;
-    const int n = drained ? 0 : claim_jobs(nf, slot, j0);
-    const uint32_t fs = take(kQFree, hf + uint32_t(lane), lane < nf) & (kQSlots - 1);
-    int ring = -1;
-    if (lane < n) {
-      // job q -> pixel q % nv, sample q / nv (q < nq <= 64 * 65535 < 2^22: div_small is exact)
-      const int x0 = Q.item[slot][0], y0 = Q.item[slot][1], vw = Q.item[slot][2], nv = Q.item[slot][3];
-      const int sbase = Q.item[slot][4];
-      const int q = j0 + lane;
-      const int qs = div_small(q, nv, 1.0f / float(nv));
-      const int p = q - qs * nv;
-      const int ly = div_small(p, vw, 1.0f / float(vw)), lx = p - ly * vw;
-      const int i = x0 + lx;
-      const int j = a.row0 + (y0 + ly) * a.row_step;
-      Xoro g;
-      g.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(i), uint32_t(sbase + qs));
-      float ju, jv;
-      g.pair(ju, jv);
-      const float u = (float(i) + ju) * cam_lds[19];  // main.cpp:278, by the reciprocal
-      const float vv = (float(j) + jv) * cam_lds[20];  // main.cpp:279
-      V3<float> co, cd;
-      get_ray<true, float>(lds_camera(cam_lds), u, vv, g, co, cd);
-      float ct;
-      int cb;
-      grid_big<kBigGroup>(a.acc, co, cd, ct, cb
-#if RTMI_STATS
-                          , cnt.bvh_stats
-#endif
-      );
-      ring = min(grid_bound<FLAT>(co, cd, ct), kQBins - 1);
-      Q.ray[0][fs] = make_float4(co.x, co.y, co.z, 1.0f);
-      Q.ray[1][fs] = make_float4(cd.x, cd.y, cd.z, 1.0f);
-      Q.ray[2][fs] = make_float4(1.0f, ct, __int_as_float((slot << 30) | (p << 24)), __int_as_float(cb));
-      Q.ray[3][fs] = make_float4(__uint_as_float(uint32_t(g.s0)), __uint_as_float(uint32_t(g.s0 >> 32)),
-                                 __uint_as_float(uint32_t(g.s1)), __uint_as_float(uint32_t(g.s1 >> 32)));
-    } else if (lane < nf) {
-      ring = kQFree;  // a free slot not needed after all: back to the free ring
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    put(ring, fs, ring >= 0);
-  };
-
-  // An item slot whose paths have all ended: its sums to the output (the
-  // floats when the item covers every sample of its tile, else the global
-  // fixed-point accumulator), its cost to the tile's, then the slot is free.
-  auto flush = [&](int s) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    const int x0 = Q.item[s][0], y0 = Q.item[s][1], vw = Q.item[s][2], nv = Q.item[s][3], tile = Q.item[s][5];
-    unsigned long long v[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      v[c] = Q.acc[s][c][lane];
-      Q.acc[s][c][lane] = 0;
-    }
-    if (lane < nv) {
-      const int ly = lane / vw, lx = lane - ly * vw;
-      const size_t o3 = (size_t(y0 + ly) * size_t(a.W) + size_t(x0 + lx)) * 3;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        if (a.block_owns_tile) out[o3 + c] = from_fixed((long long)v[c]);
-        else atomicAdd(&accum[o3 + c], v[c]);
-      }
-    }
-    if (lane == 0 && a.tile_cost) atomicAdd(&a.tile_cost[tile], q_load(&Q.segs[s]));
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    if (lane == 0) q_store(reinterpret_cast<uint32_t *>(&Q.item[s][7]), 0u);
-  };
-
-  // (counter[1] != 0: the idle watchdog fires at the first pass — fault
-  // injection for tests, RTMI_QUEUE_FAULT_INJECT)
-  uint32_t idle = counter[1] != 0u ? kQIdleMax + 1u : 0u, seen_progress = 0;
-#if RTMI_STATS
-  unsigned npass = 0;
-#endif
-#if RTMI_QUEUE_PHASES
-  // analysis build: wave cycles (s_memtime) of generation, exchange, idle
-  // passes, segment, end-of-segment work -> segments[1..5]
-  unsigned long long qc[5] = {0, 0, 0, 0, 0};
-#define QPH(k) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); qc[k] += t_ - qt; qt = t_; }
-  unsigned long long qt = __builtin_amdgcn_s_memtime();
-#else
-#define QPH(k)
-#endif
-  for (;;) {
-    // 1. camera rays into the pool while it has a batch of free slots
-    if (!drained && int(q_uniform(q_load(&Q.tail[kQFree]) - q_load(&Q.head[kQFree]))) >= 64) generate();
-    QPH(0)
-    // 2. the exchange: the fullest bin's rays for the lanes not holding one of
-    // its rays (empty lanes first: an idle lane costs more than one holding
-    // another bin's ray); lanes left without a partner keep their ray
-    {
-      uint32_t c = 0;
-      if (lane < kQBins) c = q_load(&Q.tail[lane]) - q_load(&Q.head[lane]);
-      int bs = 0;
-      uint32_t bc = uint32_t(__builtin_amdgcn_readlane(int(c), 0));
-#pragma unroll
-      for (int b = 1; b < kQBins; ++b) {
-        const uint32_t cb = uint32_t(__builtin_amdgcn_readlane(int(c), b));
-        if (cb > bc) {
-          bc = cb;
-          bs = b;
-        }
-      }
-      const bool keep = has && key == bs;
-      const unsigned long long tm = __ballot(!has), lm = __ballot(has && !keep);
-      const int nt = __popcll(tm);
-      uint32_t h = 0;
-      const int n = (tm | lm) && bc ? claim(bs, nt + __popcll(lm), h) : 0;
-      const int rank = has ? nt + q_rank(lm) : q_rank(tm);
-      const bool got = !keep && rank < n;
-      const uint32_t slot = take(bs, h + uint32_t(rank), got) & (kQSlots - 1);
-      int push_ring = -1;
-      if (got) {
-        const float4 r0 = Q.ray[0][slot], r1 = Q.ray[1][slot], r2 = Q.ray[2][slot], r3 = Q.ray[3][slot];
-        if (has) store_ray(slot);
-        push_ring = has ? key : kQFree;
-        o = mk(r0.x, r0.y, r0.z);
-        d = mk(r1.x, r1.y, r1.z);
-        T = mk(r0.w, r1.w, r2.x);
-        tmax = r2.y;
-        meta = __float_as_int(r2.z);
-        best = __float_as_int(r2.w);
-        rng.s0 = (uint64_t(__float_as_uint(r3.y)) << 32) | __float_as_uint(r3.x);
-        rng.s1 = (uint64_t(__float_as_uint(r3.w)) << 32) | __float_as_uint(r3.z);
-        has = true;
-      }
-      // the ray writes (and the reads of swapped-out slots) before the pushes
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-      put(push_ring, slot, push_ring >= 0);
-    }
-    QPH(1)
-    const unsigned long long live = __ballot(has);
-    if (live == 0) {
-      // idle passes count only while the block makes no progress: a wave
-      // waiting for a free item slot behind long paths is not stuck
-      // (ADVICE r05); progress = paths ended, all item slots
-      uint32_t prog = 0;
-      for (int k = 0; k < kQItems; ++k) prog += q_load(&Q.done[k]);
-      prog = q_uniform(prog);
-      if (prog != seen_progress) {
-        seen_progress = prog;
-        idle = 0;
-      }
-      ++idle;
-    }
-    if (__ballot(fault) || idle > kQIdleMax) {
-      if (lane == 0) {  // watchdog: reported as RT_EHIP by every call that waits for the render (check_queue_fault)
-        atomicOr(&segments[7], 1ull << 63);
-        atomicOr(&segments[8], 1ull);  // sticky: not cleared by the next pass's counters
-      }
-      break;
-    }
-    if (live == 0) {
-      if (drained) {
-        uint32_t c = 0;
-        if (lane < kQBins) c = q_load(&Q.tail[lane]) - q_load(&Q.head[lane]);
-        if (__ballot(c != 0) == 0) break;  // no rays left anywhere this wave could take
-      }
-      __builtin_amdgcn_s_sleep(4);
-      QPH(2)
-      continue;
-    }
-    idle = 0;
-    nseg = unsigned(__builtin_amdgcn_readfirstlane(int(nseg + unsigned(__popcll(live)))));
-#if RTMI_STATS
-    ++npass;
-#endif
-    // 3. one segment of every held ray, from its big-sphere result
-    bool done = false;
-    V3<float> col = mk(0.f, 0.f, 0.f);
-    if (has) done = path_segment<ACC, true>(sc, nullptr, a, o, d, T, meta, rng, col, cnt, segments, tmax, best);
-    QPH(3)
-    // 4. ended paths: colour to their item's sums; the item's last path
-    // flushes it.  Survivors: the big spheres and the bin key of their next
-    // segment.
-    int cs = 0;
-    if (done) {
-      cs = int(uint32_t(meta) >> 30);
-      const int p = (meta >> 24) & 63;
-      atomicAdd(&Q.acc[cs][0][p], (unsigned long long)to_fixed(col.x));
-      atomicAdd(&Q.acc[cs][1][p], (unsigned long long)to_fixed(col.y));
-      atomicAdd(&Q.acc[cs][2][p], (unsigned long long)to_fixed(col.z));
-      q_add(&Q.segs[cs], uint32_t(meta & 0xFFFFFF) + 1u);
-      has = false;
-    } else if (has) {
-      grid_big<kBigGroup>(a.acc, o, d, tmax, best
-#if RTMI_STATS
-                          , cnt.bvh_stats
-#endif
-      );
-      key = min(grid_bound<FLAT>(o, d, tmax), kQBins - 1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // the sums before the count
-    bool complete = false;
-    if (done) complete = int(q_add(&Q.done[cs], 1u)) + 1 == Q.item[cs][6];
-    for (unsigned long long cm = __ballot(complete); cm; cm &= cm - 1)
-      flush(__builtin_amdgcn_readlane(cs, int(__builtin_ctzll(cm))));
-    QPH(4)
-  }
-#if RTMI_QUEUE_PHASES
-  if (lane == 0)
-    for (int k = 0; k < 5; ++k) atomicAdd(&segments[1 + k], qc[k]);
-#endif
-#undef QPH
-  if (lane == 0) atomicAdd(segments, (unsigned long long)nseg);
-#if RTMI_STATS
-  if (lane == 0) atomicAdd(&segments[7], (unsigned long long)npass);  // wave passes with a live lane
-#endif
-  flush_counters(cnt, lane, segments);
-}
-#endif  // RTMI_EXPERIMENTAL (queue kernel)
 
 // Closest hit of n given rays by the brute-force loop and by the BVH
 // (validation: rt_ctx_debug_hits).  rays = {o.xyz, d.xyz} per ray.
@@ -1612,14 +1130,14 @@ __global__ __launch_bounds__(256) void debug_hit_kernel(const SpherePair *__rest
 #if RTMI_STATS
   unsigned st[4] = {0, 0, 0, 0}, bst[5] = {0, 0, 0, 0, 0};
   out_idx[2 * i] = hit_world_packed<kPairGroup>(pairs, npairs, o, d, t0, st);
-  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1, bst) : hit_world_grid<kBigGroup, acc_flat(ACC), false, acc_gmem(ACC)>(acc, o, d, t1, key, bst);
+  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1, bst) : hit_world_grid<kBigGroup, acc_flat(ACC), acc_gmem(ACC)>(acc, o, d, t1, key, bst);
 #else
   out_idx[2 * i] = hit_world_packed<kPairGroup>(pairs, npairs, o, d, t0);
 #if RTMI_TRACE_PHASES
   PhaseClock pc{{0, 0, 0}};
-  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup, acc_flat(ACC), false, acc_gmem(ACC)>(acc, o, d, t1, key, pc);
+  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup, acc_flat(ACC), acc_gmem(ACC)>(acc, o, d, t1, key, pc);
 #else
-  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup, acc_flat(ACC), false, acc_gmem(ACC)>(acc, o, d, t1, key);
+  out_idx[2 * i + 1] = ACC == 1 ? hit_world_bvh<kBigGroup>(acc, o, d, t1) : hit_world_grid<kBigGroup, acc_flat(ACC), acc_gmem(ACC)>(acc, o, d, t1, key);
 #endif
 #endif
   out_t[2 * i] = t0;
@@ -1729,10 +1247,7 @@ struct rt_ctx {
   int32_t pass_W = 0, pass_rows = 0, pass_spp = 0;
   int32_t resident_blocks = 0;             // blocks of the persistent grid (from the occupancy query)
   int32_t cu_count = 0;                    // compute units of the device
-  int32_t queue_blocks = 0;                // resident render_queue blocks for queue_lds dynamic LDS bytes
-  size_t queue_lds = 0;
   int32_t res_blocks = 0;                  // resident render_resident blocks for res_lds dynamic LDS bytes
-  bool queue_launched = false;             // a queue kernel ran on this context (check_queue_fault)
   size_t res_lds = 0;
   // BVH, built by rt_ctx_set_scene
   int32_t accel = RT_ACCEL_GRID;  // the fastest structure (brute force when the scene has none)
@@ -1803,14 +1318,8 @@ struct rt_ctx {
   bool overlap = false;
 };
 
-namespace {
-int check_queue_fault(rt_ctx *ctx, hipStream_t st);
-}  // namespace
 namespace rtmi {
 hipStream_t ctx_stream(rt_ctx *ctx) { return ctx->stream; }
-// RT_EHIP when a queue kernel's watchdog fired on this context since its last
-// whole render or accumulator reset (rt_multi's gather checks every device)
-int ctx_fault(rt_ctx *ctx) { return check_queue_fault(ctx, ctx->stream); }
 }  // namespace rtmi
 
 namespace {
@@ -1885,10 +1394,9 @@ RTMI_EXPORT int rt_ctx_create(int32_t device, rt_ctx **out) {
   ctx->device = device;
   HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&ctx->last_done, hipEventDisableTiming));
-  // [0..7] the last render's counters, [8] the queue kernel's sticky watchdog flag
-  if (int rc = dev_alloc(&ctx->segments, 9)) return rc;
-  HIP_TRY(hipMemset(ctx->segments, 0, 9 * sizeof(unsigned long long)));
-  if (int rc = dev_alloc(&ctx->counter, 2)) return rc;  // work-item counter; [1] fault injection (queue kernel)
+  if (int rc = dev_alloc(&ctx->segments, 8)) return rc;
+  HIP_TRY(hipMemset(ctx->segments, 0, 8 * sizeof(unsigned long long)));
+  if (int rc = dev_alloc(&ctx->counter, 1)) return rc;
   {
     // resident blocks per CU for the persistent grid; over-subscription is
     // harmless (extra waves start later and find the counter exhausted)
@@ -2421,19 +1929,6 @@ void launch_tw(bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx, const
 }
 
 #if RTMI_EXPERIMENTAL
-// resident blocks of the queue kernel with dyn bytes of dynamic LDS (the grid)
-int queue_resident_blocks(rt_ctx *ctx, size_t dyn) {
-  if (ctx->queue_blocks <= 0 || ctx->queue_lds != dyn) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)render_queue<8, true>, 64 * kQWaves, dyn) !=
-        hipSuccess)
-      per_cu = 0;
-    ctx->queue_blocks = std::max(1, per_cu) * std::max(1, ctx->cu_count);
-    ctx->queue_lds = dyn;
-  }
-  return ctx->queue_blocks;
-}
-
 // resident blocks of render_resident with dyn bytes of dynamic LDS
 int res_resident_blocks(rt_ctx *ctx, size_t dyn) {
   if (ctx->res_blocks <= 0 || ctx->res_lds != dyn) {
@@ -2469,17 +1964,6 @@ void launch_resident(int acc, dim3 grid, size_t lds, hipStream_t st, const rt_ct
 #undef RTMI_GO
 }
 
-template <int TW>
-void launch_queue(int acc, dim3 grid, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a,
-                  unsigned long long *accum, float *out) {
-  const size_t lds = accel_lds_bytes(a.acc, acc);
-  if (acc == 3)
-    hipLaunchKernelGGL((render_queue<TW, true>), grid, dim3(64 * kQWaves), lds, st, ctx->geom, ctx->sh0, ctx->sh1, a,
-                       accum, out, ctx->segments, ctx->counter);
-  else
-    hipLaunchKernelGGL((render_queue<TW, false>), grid, dim3(64 * kQWaves), lds, st, ctx->geom, ctx->sh0, ctx->sh1, a,
-                       accum, out, ctx->segments, ctx->counter);
-}
 #endif  // RTMI_EXPERIMENTAL
 
 template <int TW>
@@ -2513,9 +1997,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     hipStream_t s;
     ~MarkDone() { (void)hipEventRecord(c->last_done, s); }
   } mark_done{ctx, st};
-  // (a progressive pass keeps [8], the queue kernel's sticky fault flag, for
-  // rt_accum_resolve; a whole render starts without one)
-  HIP_TRY(hipMemsetAsync(ctx->segments, 0, (pass_accum ? 8 : 9) * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(ctx->segments, 0, 8 * sizeof(unsigned long long), st));
   if (nrows == 0) return RT_OK;
   // valid rows: row0 + r*row_step < H
   int32_t nvalid = 0;
@@ -2553,17 +2035,11 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
                            ? (ctx->grid.n[1] == 1 ? 3 : 2) + (ctx->grid_global ? 2 : 0)
                            : (ctx->accel != RT_ACCEL_NONE && ctx->nnodes > 0 ? 1 : 0);
   const bool bvh = acc_kind != 0;
-  // the queue kernel: grid scenes, when selected
-  // (the product build runs the automatic choice for both: they measured
-  // slower than the grid kernel; RTMI_EXPERIMENTAL builds only)
-  const bool queue = RTMI_EXPERIMENTAL && (acc_kind == 2 || acc_kind == 3) && ctx->kernel == RT_KERNEL_QUEUE && TW <= 16;
-#if RTMI_EXPERIMENTAL
-  const int64_t qblocks = queue ? queue_resident_blocks(ctx, accel_lds_bytes(accel_of(ctx, acc_kind), acc_kind)) : 0;
-#else
-  const int64_t qblocks = 0;
-#endif
-  // the resident grid kernel: accelerated scenes, when selected
-  const bool resident = RTMI_EXPERIMENTAL && bvh && !queue && ctx->kernel == RT_KERNEL_RESIDENT && TW <= 16;
+  // the resident grid kernel: accelerated scenes, when
+  // selected, in the experimental build only (measured slower than the grid
+  // kernel; the product runs the automatic choice, as for RT_KERNEL_QUEUE,
+  // whose kernel was retired in round 6: §4.6)
+  const bool resident = RTMI_EXPERIMENTAL && bvh && ctx->kernel == RT_KERNEL_RESIDENT && TW <= 16;
   // the persistent kernel runs brute-force scenes only (see the note above stage_camera)
   const bool persistent = !bvh && (ctx->kernel == RT_KERNEL_PERSISTENT ||
                                    (ctx->kernel == RT_KERNEL_AUTO && tile_samples < 6000000));
@@ -2572,11 +2048,6 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     // ~28 items per resident wave (1/8 strip: chunk 8 -> 17.5 ms, 16 -> 17.9, 32 -> 19.7)
     const int64_t waves = int64_t(ctx->resident_blocks) * kWavesPerBlock;
     chunk1 = int32_t(std::min<int64_t>(64, std::max<int64_t>(4, tile_samples / (28 * waves))));
-  } else if (chunk1 <= 0 && queue) {
-    // at least 16 items per resident block (whole tiles when there are that
-    // many tiles: the block writes the floats, no accumulator)
-    const int64_t nch = std::max<int64_t>(1, (16 * qblocks + tiles - 1) / tiles);
-    chunk1 = int32_t(std::max<int64_t>(1, (spp + nch - 1) / nch));
   } else if (chunk1 <= 0) {
     // ~60 k items of 24..125 samples (BVH, cost order, block flush; the
     // rounding below keeps a multiple of 4 items per tile): config 2 runs
@@ -2593,7 +2064,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     chunk1 = int32_t(std::min<int64_t>(125, std::max<int64_t>(item_min, tile_samples / want_items)));
   }
   if (chunk2 <= 0) chunk2 = std::max(1, chunk1 / 4);
-  if (tail < 0 || queue) tail = 0;  // automatic: no short-item phase (it measured no better)
+  if (tail < 0) tail = 0;  // automatic: no short-item phase (it measured no better)
   // at most 65535 samples per item: job indices (< 64 * chunk) stay below
   // 2^22, where the kernels' float-reciprocal division (div_small) is exact
   chunk1 = std::min({chunk1, spp, 65535});
@@ -2602,7 +2073,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   const int32_t spp1 = spp - tail;
   const int64_t grid_wpb = bvh ? GridShape<true>::waves : GridShape<false>::waves;
   int32_t nch1 = spp1 > 0 ? (spp1 + chunk1 - 1) / chunk1 : 0;
-  if (ctx->chunk <= 0 && !persistent && !queue && !resident && spp1 >= grid_wpb) {
+  if (ctx->chunk <= 0 && !persistent && !resident && spp1 >= grid_wpb) {
     // automatic grid schedule: exactly a multiple of the block's waves items
     // per tile, so a block's items share a tile and it flushes once
     // (block_flush).  chunk1 = ceil(spp1 / n1) can leave the last items of a
@@ -2634,14 +2105,14 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
   a.tiles = int32_t(tiles); a.spp1 = spp1; a.chunk1 = chunk1; a.nch1 = nch1; a.chunk2 = chunk2; a.nch2 = nch2;
   // block flush: every block's items are of one tile — both phases hold a
   // multiple of the block's waves items per tile
-  a.block_flush = !persistent && !queue && !resident && nch1 % grid_wpb == 0 && nch2 % grid_wpb == 0 && ctx->block_flush;
+  a.block_flush = !persistent && !resident && nch1 % grid_wpb == 0 && nch2 % grid_wpb == 0 && ctx->block_flush;
   a.block_owns_tile = a.block_flush && !pass_accum && nch1 == grid_wpb && nch2 == 0 && ctx->block_owns;
-  // the queue kernel: an item that covers all its tile's samples writes the floats
-  if (queue || resident) a.block_owns_tile = !pass_accum && nch1 == 1 && nch2 == 0 && ctx->block_owns;
+  // the resident kernel: an item that covers all its tile's samples writes the floats
+  if (resident) a.block_owns_tile = !pass_accum && nch1 == 1 && nch2 == 0 && ctx->block_owns;
   const bool chunked = pass_accum || nch1 + nch2 > 1;
   if (!ctx->probing) {
     const int32_t sched[8] = {TW, chunk1, nch1, nch2, a.block_flush + a.block_owns_tile, persistent ? 0 : 1,
-                              queue ? 2 : (resident ? 3 : (persistent ? 1 : 0)), acc_kind == 3 ? 2 : (acc_kind == 5 ? 4 : acc_kind)};
+                              resident ? 3 : (persistent ? 1 : 0), acc_kind == 3 ? 2 : (acc_kind == 5 ? 4 : acc_kind)};
     std::copy(sched, sched + 8, ctx->last_sched);
   }
   a.s_base = s_base;
@@ -2739,19 +2210,6 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
       default: launch_resident<16>(acc_kind, grid, lds, st, ctx, b, accum, strip); break;
     }
 #endif
-  } else if (queue) {
-#if RTMI_EXPERIMENTAL
-    // CU-resident blocks pulling work items from a global counter
-    HIP_TRY(hipMemsetAsync(ctx->counter, 0, 2 * sizeof(unsigned), st));
-    const char *inject = std::getenv("RTMI_QUEUE_FAULT_INJECT");  // (read per launch: tests toggle it)
-    if (inject && inject[0] == '1') HIP_TRY(hipMemsetAsync(ctx->counter + 1, 1, 1, st));  // tests: the watchdog path
-    ctx->queue_launched = true;
-    grid = dim3(unsigned(std::min<int64_t>(items, qblocks)));
-    switch (TW) {
-      case 8: launch_queue<8>(acc_kind, grid, st, ctx, a, accum, strip); break;
-      default: launch_queue<16>(acc_kind, grid, st, ctx, a, accum, strip); break;
-    }
-#endif
   } else if (persistent) {
     // a resident grid of waves pulling items from a global counter
     HIP_TRY(hipMemsetAsync(ctx->counter, 0, sizeof(unsigned), st));
@@ -2762,7 +2220,7 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     const int64_t wpb = bvh ? GridShape<true>::waves : GridShape<false>::waves;
     grid = dim3(unsigned((items + wpb - 1) / wpb));
   }
-  if (!queue && !resident) switch (TW) {
+  if (!resident) switch (TW) {
     case 8: launch_shape<8>(persistent, acc_kind, chunked, grid, st, ctx, a, accum, strip); break;
     case 16: launch_shape<16>(persistent, acc_kind, chunked, grid, st, ctx, a, accum, strip); break;
     case 32: launch_shape<32>(persistent, acc_kind, chunked, grid, st, ctx, a, accum, strip); break;
@@ -2812,7 +2270,6 @@ RTMI_EXPORT int rt_accum_reset(rt_ctx *ctx, int32_t W, int32_t nrows) {
   ctx->pass_spp = 0;
   if (ctx->last_stream) HIP_TRY(hipStreamSynchronize(ctx->last_stream));  // no pass still adding
   if (n) HIP_TRY(hipMemsetAsync(ctx->pass_accum, 0, n * sizeof(unsigned long long), ctx->stream));
-  HIP_TRY(hipMemsetAsync(ctx->segments + 8, 0, sizeof(unsigned long long), ctx->stream));  // (queue kernel's fault flag)
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return RT_OK;
 }
@@ -2861,8 +2318,7 @@ RTMI_EXPORT int rt_accum_resolve(rt_ctx *ctx, float *dev_sum, float *host_sum, v
     if (n) HIP_TRY(hipMemcpyAsync(host_sum, out, n * sizeof(float), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
   }
-  // a pass whose queue kernel's watchdog fired left samples out
-  return check_queue_fault(ctx, st);
+  return RT_OK;
 }
 
 // Checkpoint / resume: the raw fixed-point accumulator (W*nrows*3 int64) and
@@ -2969,25 +2425,13 @@ RTMI_EXPORT int rt_accum_load(rt_ctx *ctx, const char *path, const rt_scene *sce
   return RT_OK;
 }
 
-namespace {
-// After a queue-kernel launch has finished: its watchdog (a ring entry or an
-// idle loop that waited far past any legitimate delay) marks segments[7]
-// bit 63 and the kernel leaves early — the image is then incomplete.
-int check_queue_fault(rt_ctx *ctx, hipStream_t st) {
-  if (!ctx->queue_launched) return RT_OK;
-  unsigned long long v = 0;
-  HIP_TRY(hipMemcpyAsync(&v, ctx->segments + 8, sizeof v, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  if (v) return set_error(RT_EHIP, "queue kernel watchdog fired: the render is incomplete");
-  return RT_OK;
-}
-}  // namespace
-
 RTMI_EXPORT int rt_ctx_synchronize(rt_ctx *ctx) {
   if (!ctx) return set_error(RT_EINVAL, "null ctx");
   DeviceGuard guard(ctx->device);
   HIP_TRY(hipStreamSynchronize(ctx->stream));
-  return check_queue_fault(ctx, ctx->last_stream ? ctx->last_stream : ctx->stream);
+  // (and the stream of the last render, when it ran on a caller's stream)
+  if (ctx->last_stream && ctx->last_stream != ctx->stream) HIP_TRY(hipStreamSynchronize(ctx->last_stream));
+  return RT_OK;
 }
 
 RTMI_EXPORT int rt_render(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t spp, int32_t max_depth,
@@ -3004,7 +2448,7 @@ RTMI_EXPORT int rt_render(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t 
   if ((rc = render_rows_impl(ctx, cam, W, H, spp, max_depth, seed, 0, 1, H, ctx->scratch, ctx->stream))) return rc;
   HIP_TRY(hipMemcpyAsync(sum, ctx->scratch, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
-  return check_queue_fault(ctx, ctx->stream);
+  return RT_OK;
 }
 
 RTMI_EXPORT int rt_replay_worker(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, int32_t spp,

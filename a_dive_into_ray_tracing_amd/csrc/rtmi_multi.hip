@@ -40,7 +40,6 @@
 
 namespace rtmi {
 hipStream_t ctx_stream(rt_ctx *ctx);  // rtmi_device.hip
-int ctx_fault(rt_ctx *ctx);           // rtmi_device.hip
 }
 using namespace rtmi;
 
@@ -179,7 +178,6 @@ int gather_unpermute_body(rt_multi *m, int32_t W, int32_t H, int32_t nrows, floa
   for (int g = 0; g < G; g++) {
     (void)hipSetDevice(m->dev(g));
     if (hipStreamSynchronize(streams[g]) != hipSuccess) return set_error(RT_EHIP, "sync GPU %d", g);
-    if (int rc = rtmi::ctx_fault(m->ctx[g])) return rc;  // (a strip left incomplete by a kernel watchdog)
     if (m->mock) continue;
     ncclResult_t ae = ncclSuccess;
     ncclCommGetAsyncError(m->comm[g], &ae);

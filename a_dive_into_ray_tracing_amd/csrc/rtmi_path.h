@@ -734,11 +734,7 @@ __device__ __forceinline__ void hit_big(const Accel &acc_s, V3<float> d, float K
 // each time.  FLAT_Y: the grid has one cell layer in y (the final scene's
 // 20 x 1 x 20) — the same walk with the y axis' stepping state dropped: a y
 // face only ends the walk (5 VGPRs fewer in the loop).
-//
-// FROM_BIG (the queue kernel): the big spheres' pass was run
-// when the ray was made (grid_big): the walk starts from its result, given in
-// t_max0 / best0.
-template <int GP, bool FLAT_Y = false, bool FROM_BIG = false, bool GMEM = false>
+template <int GP, bool FLAT_Y = false, bool GMEM = false>
 __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> o, V3<float> d, float &t_hit,
                                                   uint32_t &hit_key
 #if RTMI_STATS
@@ -747,7 +743,7 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
 #if RTMI_TRACE_PHASES
                                                   , PhaseClock &pc
 #endif
-                                                  , float t_max0 = INFINITY, int32_t best0 = -1) {
+                                                  ) {
 #if RTMI_TRACE_PHASES
   const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -770,14 +766,13 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
     if constexpr (GMEM) return *reinterpret_cast<const float4 *>(gm + addr);
     else return lds_sphere(addr);
   };
-  float t_max = t_max0;
-  int32_t best_a = best0;  // the hit's record-slot key; -1: no hit yet
-  if constexpr (!FROM_BIG)
-    hit_big<GP, true, GMEM>(acc_s, d, K, a, aL, mx, my, mz, inv_a, t_max, best_a
+  float t_max = INFINITY;
+  int32_t best_a = -1;  // the hit's record-slot key; -1: no hit yet
+  hit_big<GP, true, GMEM>(acc_s, d, K, a, aL, mx, my, mz, inv_a, t_max, best_a
 #if RTMI_STATS
-                , gstats
+              , gstats
 #endif
-                );
+              );
 #if RTMI_TRACE_PHASES
   const unsigned long long tp1 = __builtin_amdgcn_s_memtime();
   pc.c[0] += tp1 - tp0;
@@ -927,53 +922,6 @@ __device__ __forceinline__ int32_t hit_world_grid(const Accel &acc_s, V3<float> 
   hit_key = best_a < 0 ? base : uint32_t(best_a);
   const int32_t k = int32_t(rd_u16(idx_base + ((hit_key - base) >> 3)));
   return best_a < 0 ? -1 : k;
-}
-
-// The big spheres' pass of hit_world_grid on its own (the queue kernel runs it
-// when a ray is made, before the ray is binned by grid_bound): t_max and the
-// record-slot key of the closest big-sphere hit (-1: none).
-template <int GP>
-__device__ __forceinline__ void grid_big(const Accel &acc_s, V3<float> o, V3<float> d, float &t_max, int32_t &best_a
-#if RTMI_STATS
-                                         , unsigned *gstats
-#endif
-                                         ) {
-  RTMI_RAY_TERMS(o, d)
-  t_max = INFINITY;
-  best_a = -1;
-  hit_big<GP, true>(acc_s, d, K, a, aL, mx, my, mz, inv_a, t_max, best_a
-#if RTMI_STATS
-              , gstats
-#endif
-              );
-}
-
-// The queue kernel's bin key: an upper bound on the cells
-// the walk will visit, known before it — the ray clipped to the grid box and
-// to the big spheres' t_max, then |dcx| + |dcy| + |dcz| + 1 between its entry
-// and exit cells (0: no cell to walk).  An ordering key only: any value
-// gives the same hit.
-template <bool FLAT_Y>
-__device__ __forceinline__ int grid_bound(V3<float> o, V3<float> d, float t_max) {
-  const GridDesc &G = rtmi_grid_desc;
-  const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
-  const float ox = -o.x * ix, oy = -o.y * iy, oz = -o.z * iz;
-  const float bx0 = __builtin_fmaf(G.g0[0], ix, ox), bx1 = __builtin_fmaf(G.g1[0], ix, ox);
-  const float by0 = __builtin_fmaf(G.g0[1], iy, oy), by1 = __builtin_fmaf(G.g1[1], iy, oy);
-  const float bz0 = __builtin_fmaf(G.g0[2], iz, oz), bz1 = __builtin_fmaf(G.g1[2], iz, oz);
-  const float tnear = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(bx0, bx1), __builtin_fminf(by0, by1)),
-                                      __builtin_fmaxf(__builtin_fminf(bz0, bz1), 0.0f));
-  const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(bx0, bx1), __builtin_fmaxf(by0, by1)),
-                                     __builtin_fminf(__builtin_fmaxf(bz0, bz1), t_max));
-  auto cell_of = [&](float p, int ax) {
-    const int c = int(__builtin_floorf((p - G.g0[ax]) * G.inv_h[ax]));
-    return c < 0 ? 0 : (c >= G.n[ax] ? G.n[ax] - 1 : c);
-  };
-  int b = 1 + abs(cell_of(__builtin_fmaf(tfar, d.x, o.x), 0) - cell_of(__builtin_fmaf(tnear, d.x, o.x), 0)) +
-          abs(cell_of(__builtin_fmaf(tfar, d.z, o.z), 2) - cell_of(__builtin_fmaf(tnear, d.z, o.z), 2));
-  if constexpr (!FLAT_Y)
-    b += abs(cell_of(__builtin_fmaf(tfar, d.y, o.y), 1) - cell_of(__builtin_fmaf(tnear, d.y, o.y), 1));
-  return tnear <= tfar ? b : 0;
 }
 
 template <int GP>

@@ -374,7 +374,7 @@ def timed_kernel_symbol(sched, flat):
     if kind == 0:
         chunked = int(sched["items_per_tile"] + sched["tail_items_per_tile"] > 1)
         return f"render_kernelILi{tw}ELb{chunked}ELi{a}E"
-    return None  # (persistent / queue: no committed record)
+    return None  # (the persistent kernel: no committed record)
 
 
 def pmc_guard(record, lib_path, symbol):
@@ -946,7 +946,7 @@ def main():
                 "walk_lane_utilisation": round(counts["node_visits"] / max(1, 64 * counts["node_iterations_wave"]), 4),
                 "leaf_lane_utilisation": round(counts["leaf_sphere_tests"] / max(1, 64 * counts["leaf_sphere_iterations_wave"]), 4),
             }
-            if counts.get("wave_passes"):  # the queue kernel's stats build counts its wave passes
+            if counts.get("wave_passes"):  # (a stats build that counts wave passes)
                 roof["counts"]["live_lanes_per_pass"] = round(counts["segments"] / counts["wave_passes"], 2)
         # Context beside the algorithmic fraction, from the committed PMC passes
         # of the same kernel on the same workload (tools/profile.sh,

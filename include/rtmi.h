@@ -146,13 +146,11 @@ int rt_ctx_set_overlap(rt_ctx *ctx, int32_t overlapped);
  * BVH the grid kernel runs, which measured faster.
  * RT_KERNEL_GRID: one wave per work item.  RT_KERNEL_AUTO (default):
  * persistent for brute-force strips (fewer than 6e6 tile-samples), grid
- * otherwise.  RT_KERNEL_QUEUE: CU-resident 16-wave blocks that share an LDS
- * pool of rays binned by the length of their next grid walk (grid scenes,
- * tiles of 8 or 16 columns; otherwise as RT_KERNEL_AUTO).
- * RT_KERNEL_RESIDENT: CU-resident 16-wave blocks whose waves each run the grid
- * kernel's loop over work items taken from a global counter (accelerated
- * scenes, tiles of 8 or 16 columns; otherwise as RT_KERNEL_AUTO; DESIGN.md
- * §4.7).  All give bit-identical images. */
+ * otherwise.  RT_KERNEL_QUEUE (round 5's LDS ray-queue kernel, retired in
+ * round 6: DESIGN.md §4.6) and RT_KERNEL_RESIDENT (CU-resident blocks over a
+ * global work counter, DESIGN.md §4.7: built only into the experimental
+ * library, lib/librtmi_experimental.so) run RT_KERNEL_AUTO in librtmi.so —
+ * both measured slower than the grid kernel.  All give bit-identical images. */
 enum { RT_KERNEL_GRID = 0, RT_KERNEL_PERSISTENT = 1, RT_KERNEL_AUTO = 2, RT_KERNEL_QUEUE = 3, RT_KERNEL_RESIDENT = 4 };
 int rt_ctx_set_kernel(rt_ctx *ctx, int32_t kind);
 

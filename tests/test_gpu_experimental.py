@@ -1,12 +1,11 @@
-"""The kernels that measured slower than the grid kernel — the queue kernel
-(RT_KERNEL_QUEUE) and the resident grid kernel
-(RT_KERNEL_RESIDENT, §4.7) — live only in the experimental build
+"""The resident grid kernel (RT_KERNEL_RESIDENT), measured
+slower than the grid kernel, lives only in the experimental build
 (lib/librtmi_experimental.so, `make -C a_dive_into_ray_tracing_amd/csrc
-experimental`).  The product library runs the automatic choice for both
-kinds (same image); the experimental build's own suite
-(tests/experimental/exp_gpu_*.py: bit-exact against the oracle and the grid
-kernel, the queue kernel's watchdog fault reporting) runs in ONE child
-process, since a process loads one library."""
+experimental`); the queue kernel (RT_KERNEL_QUEUE, §4.6) was retired.  The
+product library runs the automatic choice for both kinds (same image); the
+experimental build's own suite (tests/experimental/exp_gpu_resident.py:
+bit-exact against the oracle and the grid kernel) runs in ONE child process,
+since a process loads one library."""
 import os
 import subprocess
 import sys
@@ -39,11 +38,9 @@ def test_product_runs_the_automatic_kernel_for_experimental_kinds(kind):
 @pytest.mark.skipif(not os.path.exists(EXP_LIB), reason="experimental build absent (make ... experimental)")
 def test_experimental_build_suite():
     env = dict(os.environ, RTMI_LIBRARY=EXP_LIB)
-    env.pop("RTMI_QUEUE_FAULT_INJECT", None)
     out = os.path.join(REPO, "gpurun_out")
     os.makedirs(out, exist_ok=True)
     p = subprocess.run([sys.executable, "-u", "-m", "pytest", "-x", "-v", "-p", "no:cacheprovider",
-                        os.path.join(REPO, "tests", "experimental", "exp_gpu_queue.py"),
                         os.path.join(REPO, "tests", "experimental", "exp_gpu_resident.py")],
                        capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
     with open(os.path.join(out, "experimental_suite.log"), "w") as f:

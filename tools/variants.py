@@ -20,7 +20,6 @@ LIB = os.path.join(REPO, "a_dive_into_ray_tracing_amd", "lib")
 VARIANTS = {
     "trace": ("variant", "-DRTMI_TRACE=1 -DRTMI_TRACE_PHASES=1"),  # per-wave timeline + phase clocks (tools/trace_run.py)
     "wavetrace": ("variant", "-DRTMI_TRACE=1"),  # per-wave timeline only (tools/gpu_trace_ab.sh)
-    "qph": ("variant", "-DRTMI_EXPERIMENTAL=1 -DRTMI_QUEUE_PHASES=1"),  # queue kernel phase clocks (tools/queue_phases.py)
     "nwph": ("nwvariant", "-DRTMI_NW_PHASES=1"),  # Next-Week phase clocks (tools/nw_phases.py)
 }
 

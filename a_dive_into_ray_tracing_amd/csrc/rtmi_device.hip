@@ -1306,6 +1306,13 @@ struct rt_ctx {
   int32_t probe_mode = std::getenv("RTMI_ORDER_PROBE") ? std::atoi(std::getenv("RTMI_ORDER_PROBE")) : 1;
   // samples per pixel of the probe (RTMI_PROBE_SPP, for A/B; 0 = automatic)
   int32_t probe_spp = std::getenv("RTMI_PROBE_SPP") ? std::atoi(std::getenv("RTMI_PROBE_SPP")) : 0;
+  // path depth limit of the probe (RTMI_PROBE_DEPTH overrides, for A/B and
+  // tests; 0 = the default, 8): a tile's cost shows by depth 8 (depth 2 would
+  // hide the glass spheres' long paths), and the probe's launch ends sooner
+  // without the rare 50-segment paths (one rank's 1/8 strip of config 2,
+  // one-shot 2.81 ms with 1 spp to depth 8 against 2.96 with 2 spp to depth
+  // 50; the frame 19.57 vs 19.64; profiles/r06/oneshot/)
+  int32_t probe_depth = std::getenv("RTMI_PROBE_DEPTH") ? std::atoi(std::getenv("RTMI_PROBE_DEPTH")) : 0;
   bool probing = false;
   // automatic item size of the grid kernel: ~want_items items of item_min..125
   // samples; 0 = the default of the launch mode below (RTMI_WANT_ITEMS /
@@ -2167,14 +2174,15 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
       }
     }
     const bool have_map = ctx->cost_valid && std::equal(key, key + 6, ctx->cost_key);
-    // Probe: 1 sample per pixel (2 from 256 spp up) rendered into the output
-    // strip (overwritten by this render) counts world.hit per tile, about
-    // 1/250 of the render's work; the render then dispatches by those counts.
+    // Probe: 1 sample per pixel, paths cut at depth 8, rendered into the
+    // output strip (overwritten by this render) counts world.hit per tile,
+    // under 1/500 of the render's work; the render then dispatches by those counts.
     if (!ctx->probing && strip && !pass_accum && spp >= 16 &&
         (ctx->probe_mode == 2 || (ctx->probe_mode == 1 && !have_map))) {
       ctx->probing = true;
-      const int32_t pspp = ctx->probe_spp > 0 ? std::min(ctx->probe_spp, spp) : (spp >= 256 ? 2 : 1);
-      const int rc = render_rows_impl(ctx, cam, W, H, pspp, max_depth, seed, row0, row_step, nrows, strip,
+      const int32_t pspp = ctx->probe_spp > 0 ? std::min(ctx->probe_spp, spp) : 1;
+      const int32_t pdepth = std::min(ctx->probe_depth > 0 ? ctx->probe_depth : 8, max_depth);
+      const int rc = render_rows_impl(ctx, cam, W, H, pspp, pdepth, seed, row0, row_step, nrows, strip,
                                       st, s_base, nullptr);
       ctx->probing = false;
       if (rc) return rc;

@@ -983,7 +983,7 @@ def main():
             "metric": METRIC,
             "value": round(value, 3),
             # the reference's use case renders once (main.cpp:292-360): a render
-            # with no cost map of its layout runs a 1-2 spp probe pass first
+            # with no cost map of its layout runs a 1-spp, depth-8 probe pass first
             # (kernel time of that one render, HIP events); the timed steps
             # above reuse the previous identical render's map (config.timed_steps)
             "one_shot_msamples_per_s": (one_shot or {}).get("msamples_per_s"),
@@ -1010,7 +1010,7 @@ def main():
                 "overlap_schedule": bool(npipe > 1 and args.steps >= 8 and not STUB),
                 "timed_steps": ("each step re-renders the same workload; with ordering 'cost' it dispatches tiles by the "
                                 "previous identical render's per-tile cost map (RT_ORDER_COST): the first render of a "
-                                "layout (warmup) pays a 1-2 spp probe pass instead, see one_shot_msamples_per_s"
+                                "layout (warmup) pays a 1-spp probe pass instead, see one_shot_msamples_per_s"
                                 if args.ordering == "cost" else "image-order dispatch, no cost map"),
             },
             "roofline": roof,

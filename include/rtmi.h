@@ -175,8 +175,9 @@ enum { RT_ACCEL_NONE = 0, RT_ACCEL_BVH = 1, RT_ACCEL_GRID = 2 };
  * calls per tile and dispatches its tiles most-expensive-first (a GPU radix
  * sort of per-tile counts), so the end of the launch is cheap work.  The
  * counts come from the previous render with the same tile layout, or — when
- * there is none (a one-shot render) — from a probe pass of 1-2 samples per
- * pixel run first on the same stream (~1/250 of the work).  RT_ORDER_NONE:
+ * there is none (a one-shot render) — from a probe pass of 1 sample per
+ * pixel with paths cut at depth 8, run first on the same stream (under 1/500
+ * of the work).  RT_ORDER_NONE:
  * tiles in image order.  Never changes the image. */
 enum { RT_ORDER_NONE = 0, RT_ORDER_COST = 1 };
 int rt_ctx_set_ordering(rt_ctx *ctx, int32_t ordering);

@@ -726,15 +726,17 @@ def test_cost_ordered_dispatch_same_image(kernel, accel, final_world, final_rend
     assert np.array_equal(ordered, want)
 
 
-@pytest.mark.parametrize("probe_spp", ["1", "2", "5"])
-def test_probe_samples_do_not_change_the_image(probe_spp, final_world, monkeypatch):
-    """The cost probe of a one-shot render (RTMI_PROBE_SPP samples per pixel
-    into the output, counting world.hit per tile) only orders the tiles: the
-    image and the world.hit count of the render equal the unordered render's
-    and the oracle's, whatever the probe's sample count."""
+@pytest.mark.parametrize("probe_spp,probe_depth", [("1", "0"), ("2", "0"), ("5", "0"), ("1", "50"), ("2", "2")])
+def test_probe_samples_do_not_change_the_image(probe_spp, probe_depth, final_world, monkeypatch):
+    """The cost probe of a one-shot render (RTMI_PROBE_SPP samples per pixel,
+    paths cut at RTMI_PROBE_DEPTH segments, into the output, counting
+    world.hit per tile) only orders the tiles: the image and the world.hit
+    count of the render equal the unordered render's and the oracle's,
+    whatever the probe's sample count and depth (0: the default, 8)."""
     W, H, S = 64, 40, 20
     cam = rt.final_camera(W / H)
     monkeypatch.setenv("RTMI_PROBE_SPP", probe_spp)
+    monkeypatch.setenv("RTMI_PROBE_DEPTH", probe_depth)
     r = rt.Renderer(final_world, 0)
     try:
         r.set_accel("grid")

@@ -29,7 +29,7 @@ def gather_strips(strip, rank, world, dst=0, async_op=False):
     wait for the collective, without blocking the host)."""
     import torch.distributed as dist
 
-    if world == 1:
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):  # no process group: nothing to gather
         return ([strip], None) if async_op else [strip]
     bufs = [strip.new_empty(strip.shape) for _ in range(world)] if rank == dst else None
     work = dist.gather(strip, gather_list=bufs, dst=dst, async_op=async_op)

@@ -177,7 +177,7 @@ def dist_setup(torch, dist):
     if STUB:  # CPU rehearsal: no device at all
         if backend != "gloo":
             raise SystemExit("bench: RTMI_BENCH_STUB=1 needs RTMI_DIST_BACKEND=gloo")
-        if world_size > 1:
+        if world_size > 1 or FORCE_DIST:
             init_group(dist, "gloo")
         cpu = torch.device("cpu")
         return world_size, rank, -1, cpu, cpu
@@ -187,7 +187,7 @@ def dist_setup(torch, dist):
     device = local_rank % max(1, ndev) if backend == "gloo" else local_rank
     torch.cuda.set_device(device)
     dev = torch.device("cuda", device)
-    if world_size > 1:
+    if world_size > 1 or FORCE_DIST:
         if backend == "gloo":
             init_group(dist, "gloo")
         else:
@@ -205,6 +205,11 @@ def dist_setup(torch, dist):
 STUB = os.environ.get("RTMI_BENCH_STUB") == "1"
 # tests/test_bench_dist.py only (stub runs): rank RTMI_BENCH_STALL_RANK sleeps
 # RTMI_BENCH_STALL_S seconds before each gather, past the collective timeout
+# RTMI_DIST_FORCE=1 under a launcher (WORLD_SIZE set): the process group and
+# every collective of the N > 1 path run at world size 1 too (a one-rank
+# RCCL rehearsal of the exact calls the N-GPU run makes on one GPU; RCCL
+# refuses two ranks on one device).  The line says so (config.dist_rehearsal).
+FORCE_DIST = os.environ.get("RTMI_DIST_FORCE") == "1" and "WORLD_SIZE" in os.environ
 STALL_RANK = int(os.environ.get("RTMI_BENCH_STALL_RANK", "-1")) if STUB else -1
 STALL_S = float(os.environ.get("RTMI_BENCH_STALL_S", "0"))
 
@@ -634,6 +639,7 @@ def main():
 
     world_size, rank, local_rank, dev, coll = dist_setup(torch, dist)
     N = world_size
+    DIST = N > 1 or FORCE_DIST  # the N > 1 path: process group, gathers, barriers, max over ranks
 
     world = rt.random_scene()
     cam = rt.final_camera(W / H)
@@ -664,7 +670,7 @@ def main():
     # while step k's render or gather still uses the other (a buffer is
     # rendered into again only after its gather is done); buffer b is always
     # rendered by context b % npipe on its stream
-    strips = [strip] + [torch.empty_like(strip) for _ in range(max(npipe, 2 if N > 1 else 1) - 1)]
+    strips = [strip] + [torch.empty_like(strip) for _ in range(max(npipe, 2 if DIST else 1) - 1)]
     tw = args.tile_w or rt.auto_tile_w(W, -(-(H - row0) // row_step) if row0 < H else 0)  # reported tile shape
     gathered = None
     destroy_streams = None
@@ -724,7 +730,7 @@ def main():
             render_into((row0, row_step, nrows), buf, c)
         if STALL_RANK == rank:  # test only: this rank stalls before its gather
             time.sleep(STALL_S)
-        if N > 1:  # the single exchange step: strips -> rank 0 over RCCL/xGMI, overlapping the next render
+        if DIST:  # the single exchange step: strips -> rank 0 over RCCL/xGMI, overlapping the next render
             src = buf if coll.type == dev.type else buf.cpu()  # (gloo rehearsal: host copy)
             bufs, work = collective(f"gather of step {nstep[0]}'s strips", rdist.gather_strips, src, rank, N, dst=0,
                                     async_op=True)
@@ -744,7 +750,7 @@ def main():
     sync()
     if not STUB:
         torch.cuda.set_stream(streams[0])
-    if N > 1:
+    if DIST:
         collective("barrier before the timed region", dist.barrier)
     sync()
     t0 = time.perf_counter()
@@ -752,13 +758,13 @@ def main():
         step(True)
     drain()
     sync()
-    if N > 1:
+    if DIST:
         collective("barrier after the timed region", dist.barrier)
     sync()
     elapsed = my_elapsed = time.perf_counter() - t0
     if not STUB:
         torch.cuda.set_stream(streams[0])
-    if N > 1:
+    if DIST:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
         collective("all_reduce(max) of the timed region", dist.all_reduce, t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -774,7 +780,7 @@ def main():
     # single-launch schedule, not the overlap hint of the timed steps
     r.set_overlap(False)
     dist_info = None
-    if N > 1:
+    if DIST:
         # the gather's own time (outside the timed region, where it overlaps
         # the next render): one more step with a blocking gather between HIP
         # events on the render's stream (from the end of this rank's render to
@@ -813,7 +819,7 @@ def main():
     # whole frame, bit for bit (every pixel's stream is keyed by its
     # coordinates, so the partition must not change a single value)
     gather_check = None
-    if N > 1 and not args.timed_only:
+    if DIST and not args.timed_only:
         if rank == 0:
             full = torch.empty((H, W, 3), dtype=torch.float32, device=dev)
             e0, e1 = timed_render((0, 1, H), full)
@@ -833,7 +839,7 @@ def main():
     one_shot = None
     if args.ordering == "cost" and not args.timed_only:
         r.set_ordering("cost")  # forgets the previous render's cost map
-        if N > 1:
+        if DIST:
             # One render as the reference's use case does it, on every rank: from
             # a common start (barrier) to the end of the blocking gather of the
             # strips at rank 0, max over ranks
@@ -854,7 +860,7 @@ def main():
         e2, e3 = timed_render()
         sync()
         one_shot = {"probe_ordered_ms": round(e0.elapsed_time(e1), 3), "image_order_ms": round(e2.elapsed_time(e3), 3)}
-        if N == 1:  # this rank's rows are the whole workload (or the --strip-of strip)
+        if not DIST:  # this rank's rows are the whole workload (or the --strip-of strip)
             one_shot["msamples_per_s"] = round(nrows_valid * W * SPP / (one_shot["probe_ordered_ms"] * 1e-3) / 1e6, 3)
         else:  # the whole frame over N GPUs: render with its probe + gather, wall clock, max over ranks
             one_shot["wall_ms_max_rank"] = round(os_wall * 1e3, 3)
@@ -1001,7 +1007,7 @@ def main():
             "config": {
                 "workload": f"rtiow_final_{W}x{H}_{SPP}spp_depth{DEPTH}",
                 "width": W, "height": H, "spp": SPP, "max_depth": DEPTH, "seed": SEED, "spheres": len(world),
-                "partition": "interleaved rows, one RCCL gather" if N > 1 else "single GPU",
+                "partition": "interleaved rows, one RCCL gather" if DIST else "single GPU",
                 "tile": f"{tw}x{64 // tw}" + ("" if args.tile_w else " (auto)"),
                 "kernel": args.kernel,
                 "accel": args.accel,
@@ -1019,18 +1025,21 @@ def main():
         }
         if STUB:
             line["stub"] = True
+        if FORCE_DIST and N == 1:
+            line["config"]["dist_rehearsal"] = ("RTMI_DIST_FORCE: one rank through every collective of the N > 1 "
+                                                "path (gathers, barriers, max over ranks, gather check, one-shot)")
         if dist_info is not None:
             line["dist"] = dist_info
         if gather_check is not None:
             line["gather_check"] = gather_check
-        if N == 1 and not args.no_cpu_baseline:
+        if not DIST and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)
         if gather_check is not None and not gather_check["bit_exact_vs_1gpu_frame"]:
             dist.destroy_process_group()
             close_all(rs, destroy_streams)
             sys.exit(3)
-    if N > 1:  # (before the streams its collectives ran on are destroyed)
+    if DIST:  # (before the streams its collectives ran on are destroyed)
         dist.destroy_process_group()
     close_all(rs, destroy_streams)
 

@@ -85,3 +85,38 @@ def test_stalled_rank_fails_fast_with_rank_and_collective_named(tmp_path):
     assert took < 100, took  # not the stall's 120 s, nor torch's 10-minute default
     assert p.stdout.strip() == "", p.stdout[-2000:]
     assert "bench: rank 0 of 2: collective failed (timeout 4 s): gather of step 1's strips" in p.stderr, p.stderr[-3000:]
+
+
+def test_forced_one_rank_runs_the_n_rank_path(tmp_path):
+    """RTMI_DIST_FORCE=1 under the launcher at world size 1: the process group
+    and every collective of the N > 1 path run with one rank (the GPU box's
+    one-rank RCCL rehearsal, tools/gpu_rccl_one_rank.sh); the line says so and
+    carries the dist fields, the gather check and the one-shot wall figure."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(RTMI_DIST_BACKEND="gloo", RTMI_BENCH_STUB="1", OMP_NUM_THREADS="1", RTMI_DIST_FORCE="1")
+    cmd = bench.launch_command(1, ["--gpus", "1", "--steps", "3", "--warmup", "1"], bench.free_port())
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = p.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and "RTMI_DIST_FORCE" in d["config"]["dist_rehearsal"]
+    assert d["config"]["partition"] == "interleaved rows, one RCCL gather"
+    assert d["dist"]["world_size"] == 1 and d["dist"]["segments_per_rank"] == [1200 * 800 * 500]
+    assert d["gather_check"]["bit_exact_vs_1gpu_frame"] is True
+    assert d["one_shot"]["wall_ms_max_rank"] > 0
+    assert "cpu_baseline" not in d
+
+
+def test_force_without_launcher_is_the_plain_path(tmp_path):
+    """RTMI_DIST_FORCE without a launcher environment changes nothing."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(RTMI_DIST_BACKEND="gloo", RTMI_BENCH_STUB="1", OMP_NUM_THREADS="1", RTMI_DIST_FORCE="1")
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads(p.stdout.splitlines()[-1])
+    assert "dist" not in d and "dist_rehearsal" not in d["config"] and d["config"]["partition"] == "single GPU"

@@ -210,6 +210,8 @@ STUB = os.environ.get("RTMI_BENCH_STUB") == "1"
 # RCCL rehearsal of the exact calls the N-GPU run makes on one GPU; RCCL
 # refuses two ranks on one device).  The line says so (config.dist_rehearsal).
 FORCE_DIST = os.environ.get("RTMI_DIST_FORCE") == "1" and "WORLD_SIZE" in os.environ
+DIST_REHEARSAL = ("RTMI_DIST_FORCE: one rank through every collective of the N > 1 path (gathers, barriers, max "
+                  "over ranks, gather check, one-shot)")
 STALL_RANK = int(os.environ.get("RTMI_BENCH_STALL_RANK", "-1")) if STUB else -1
 STALL_S = float(os.environ.get("RTMI_BENCH_STALL_S", "0"))
 
@@ -1026,8 +1028,7 @@ def main():
         if STUB:
             line["stub"] = True
         if FORCE_DIST and N == 1:
-            line["config"]["dist_rehearsal"] = ("RTMI_DIST_FORCE: one rank through every collective of the N > 1 "
-                                                "path (gathers, barriers, max over ranks, gather check, one-shot)")
+            line["config"]["dist_rehearsal"] = DIST_REHEARSAL
         if dist_info is not None:
             line["dist"] = dist_info
         if gather_check is not None:
@@ -1103,6 +1104,7 @@ def bench_nw(args):
     from a_dive_into_ray_tracing_amd import dist as rdist
 
     N, rank, local_rank, dev, coll = dist_setup(torch, dist)
+    DIST = N > 1 or FORCE_DIST  # (as in main)
     if args.workload == "nw_motion_blur":
         which, Wn, Hn, spp = 1, 1200, 800, args.nw_spp or 500
         earth = None
@@ -1130,25 +1132,25 @@ def bench_nw(args):
         if record:
             e1.record(stream)
             ev.append((e0, e1))
-        if N > 1:
+        if DIST:
             collective("gather of the strips", rdist.gather_strips, strip if coll.type == "cuda" else strip.cpu(), rank, N,
                        dst=0)
 
     for _ in range(args.warmup):
         step(False)
     torch.cuda.synchronize(dev)
-    if N > 1:
+    if DIST:
         collective("barrier before the timed region", dist.barrier)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
     torch.cuda.synchronize(dev)
-    if N > 1:
+    if DIST:
         collective("barrier after the timed region", dist.barrier)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    if N > 1:
+    if DIST:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
         collective("all_reduce(max) of the timed region", dist.all_reduce, t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -1181,7 +1183,7 @@ def bench_nw(args):
             "data": "synthetic: the reference's scene regenerated from a restated curand XORWOW (curand_init(1984,0,0))",
             "config": {"workload": f"{args.workload}_{Wn}x{Hn}_{spp}spp_depth{DEPTH}", "scene": which, "width": Wn,
                        "height": Hn, "spp": spp, "max_depth": DEPTH, "seed": SEED,
-                       "partition": "interleaved rows, one RCCL gather" if N > 1 else "single GPU",
+                       "partition": "interleaved rows, one RCCL gather" if DIST else "single GPU",
                        "accel": accel["accel"], "grid_dims": list(accel["dims"]), "grid_max_cell": accel["max_cell"],
                        "brute_force_objects": accel["n_big"]},
             "roofline": {
@@ -1208,11 +1210,13 @@ def bench_nw(args):
         }
         if why:
             line["roofline"]["note"] = why
-        if N == 1 and not args.no_cpu_baseline:
+        if FORCE_DIST and N == 1:
+            line["config"]["dist_rehearsal"] = DIST_REHEARSAL
+        if not DIST and not args.no_cpu_baseline:
             line["cpu_baseline"] = nw_cpu_baseline(scene.flat(), cam, which, Wn, Hn)
         print(json.dumps(line), flush=True)
     r.close()
-    if N > 1:
+    if DIST:
         dist.destroy_process_group()
 
 

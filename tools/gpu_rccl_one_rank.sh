@@ -3,7 +3,8 @@
 # ranks on one device): torch.distributed.run with one rank, backend nccl,
 # RTMI_DIST_FORCE=1, so the process group, the async gathers on the CU-masked
 # streams, the barriers, the max-over-ranks reductions, the gather check and
-# the one-shot gather all run through RCCL.  Then the same with --pipeline 1.
+# the one-shot gather all run through RCCL.  Then the same with --pipeline 1,
+# and the Next-Week bench path.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -16,10 +17,11 @@ run() {  # name, bench args...
   python - $OUT/$name.json <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().splitlines()[-1])
-di, gc, os_ = d["dist"], d.get("gather_check"), d["one_shot"]
-print(sys.argv[1], d["value"], d["ms_per_step"], di["backend"], di["world_size"], di["gather_ms_per_rank"],
-      gc and gc["bit_exact_vs_1gpu_frame"], os_.get("wall_ms_max_rank"), d["one_shot_msamples_per_s"],
-      d["config"]["pipeline"], d["config"].get("dist_rehearsal") is not None)
+di, gc, os_ = d.get("dist") or {}, d.get("gather_check"), d.get("one_shot") or {}
+print(sys.argv[1], d["value"], d["ms_per_step"], di.get("backend"), di.get("world_size"), di.get("gather_ms_per_rank"),
+      gc and gc["bit_exact_vs_1gpu_frame"], os_.get("wall_ms_max_rank"), d.get("one_shot_msamples_per_s"),
+      d["config"].get("pipeline"), d["config"].get("dist_rehearsal") is not None)
 PY
 }
-run p2 --steps 20 --warmup 5 && run p1 --steps 10 --warmup 2 --pipeline 1
+run p2 --steps 20 --warmup 5 && run p1 --steps 10 --warmup 2 --pipeline 1 &&
+  run nw --workload nw_motion_blur --nw-spp 50 --steps 3 --warmup 1

@@ -210,6 +210,17 @@ STUB = os.environ.get("RTMI_BENCH_STUB") == "1"
 # RCCL rehearsal of the exact calls the N-GPU run makes on one GPU; RCCL
 # refuses two ranks on one device).  The line says so (config.dist_rehearsal).
 FORCE_DIST = os.environ.get("RTMI_DIST_FORCE") == "1" and "WORLD_SIZE" in os.environ
+# Where a timed step's gather runs (A/B knob RTMI_BENCH_GATHER=inline|side):
+# "side" issues it as an async collective (torch's NCCL stream, joined by a
+# stream wait before its buffer is rendered into again); "inline" issues it
+# as a synchronous collective, which this torch runs on the caller's current
+# stream: the render's own stream and hardware queue, after the render.  With
+# two contexts that puts one communicator's collectives on two streams, whose
+# kernels may then run out of issue order (NCCL forbids it: a possible hang at
+# N > 1), so "inline" is an A/B mode for one-rank runs only (main() refuses it
+# otherwise).  Measured at one rank (profiles/r06/rccl_one_rank/): 1/8 strip
+# 2.58 (inline) vs 2.66 (side) vs 2.53 ms without gathers.
+GATHER_INLINE = os.environ.get("RTMI_BENCH_GATHER", "side") == "inline"
 DIST_REHEARSAL = ("RTMI_DIST_FORCE: one rank through every collective of the N > 1 path (gathers, barriers, max "
                   "over ranks, gather check, one-shot)")
 STALL_RANK = int(os.environ.get("RTMI_BENCH_STALL_RANK", "-1")) if STUB else -1
@@ -642,6 +653,9 @@ def main():
     world_size, rank, local_rank, dev, coll = dist_setup(torch, dist)
     N = world_size
     DIST = N > 1 or FORCE_DIST  # the N > 1 path: process group, gathers, barriers, max over ranks
+    if GATHER_INLINE and N > 1 and args.pipeline > 1:
+        sys.exit("bench: RTMI_BENCH_GATHER=inline with --pipeline > 1 is a one-rank A/B mode (one communicator on "
+                 "two streams may hang at N > 1)")
 
     world = rt.random_scene()
     cam = rt.final_camera(W / H)
@@ -668,11 +682,19 @@ def main():
         row0, row_step, nrows = rdist.strip_rows(H, 0, args.strip_of)
     nrows_valid = len(range(row0, H, row_step))  # rows of this strip inside the image
     strip = torch.empty((nrows, W, 3), dtype=torch.float32, device=dev)
-    # two strip buffers (N > 1 or two contexts): step k+1 renders into one
-    # while step k's render or gather still uses the other (a buffer is
-    # rendered into again only after its gather is done); buffer b is always
-    # rendered by context b % npipe on its stream
-    strips = [strip] + [torch.empty_like(strip) for _ in range(max(npipe, 2 if DIST else 1) - 1)]
+    # Strip buffers: one per context, two per context with gathers (N > 1).
+    # Buffer b is always rendered by context b % npipe on its stream, and
+    # rendered into again only after its previous gather is done; with two
+    # per context a render waits for the gather of the step npipe * 2 back,
+    # not of the step before on its stream, so a gather that waits for
+    # CU slots (or for a slower rank) does not hold up the next render of
+    # its context (one-rank RCCL rehearsal: frame 19.26 -> 19.09 ms per step,
+    # the 1/8 strip unchanged at 2.66; RTMI_BENCH_STRIP_BUFS overrides the
+    # count for that A/B).
+    nbuf = int(os.environ.get("RTMI_BENCH_STRIP_BUFS", "0")) or (2 * npipe if DIST else npipe)
+    if nbuf % npipe:
+        sys.exit(f"bench: RTMI_BENCH_STRIP_BUFS={nbuf} is not a multiple of --pipeline {npipe}")
+    strips = [strip] + [torch.empty_like(strip) for _ in range(nbuf - 1)]
     tw = args.tile_w or rt.auto_tile_w(W, -(-(H - row0) // row_step) if row0 < H else 0)  # reported tile shape
     gathered = None
     destroy_streams = None
@@ -718,6 +740,7 @@ def main():
         gathered = bufs
 
     def step(record):
+        nonlocal gathered
         b = nstep[0] % len(strips)
         c = b % npipe  # this step's context and stream
         nstep[0] += 1
@@ -734,9 +757,12 @@ def main():
             time.sleep(STALL_S)
         if DIST:  # the single exchange step: strips -> rank 0 over RCCL/xGMI, overlapping the next render
             src = buf if coll.type == dev.type else buf.cpu()  # (gloo rehearsal: host copy)
-            bufs, work = collective(f"gather of step {nstep[0]}'s strips", rdist.gather_strips, src, rank, N, dst=0,
-                                    async_op=True)
-            pend[b] = (nstep[0], bufs, work, src)  # the source stays referenced until the gather is done
+            if GATHER_INLINE:
+                gathered = collective(f"gather of step {nstep[0]}'s strips", rdist.gather_strips, src, rank, N, dst=0)
+            else:
+                bufs, work = collective(f"gather of step {nstep[0]}'s strips", rdist.gather_strips, src, rank, N,
+                                        dst=0, async_op=True)
+                pend[b] = (nstep[0], bufs, work, src)  # the source stays referenced until the gather is done
 
     def drain():  # every gather in flight, in the order issued (the last one's strips are `gathered`)
         for b in sorted(pend, key=lambda k: pend[k][0]):

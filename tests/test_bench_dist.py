@@ -120,3 +120,14 @@ def test_force_without_launcher_is_the_plain_path(tmp_path):
     assert p.returncode == 0, p.stderr[-3000:]
     d = json.loads(p.stdout.splitlines()[-1])
     assert "dist" not in d and "dist_rehearsal" not in d["config"] and d["config"]["partition"] == "single GPU"
+
+
+def test_inline_gather_refused_with_two_contexts_at_n_ranks(tmp_path):
+    """RTMI_BENCH_GATHER=inline would put one communicator's gathers on two
+    streams at N > 1 (a possible hang): refused before any rank renders."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(RTMI_DIST_BACKEND="gloo", RTMI_BENCH_STUB="1", OMP_NUM_THREADS="1", RTMI_BENCH_GATHER="inline")
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert p.returncode != 0 and p.stdout.strip() == ""
+    assert "one-rank A/B mode" in p.stderr, p.stderr[-2000:]

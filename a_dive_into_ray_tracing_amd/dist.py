@@ -21,18 +21,19 @@ def strip_rows(H, rank, world):
     return rank, world, (H + world - 1) // world
 
 
-def gather_strips(strip, rank, world, dst=0, async_op=False):
+def gather_strips(strip, rank, world, dst=0, async_op=False, group=None):
     """Gather every rank's strip tensor to `dst` (one collective).  Returns the
     list of strips on dst, None elsewhere; with async_op, (that list, the
     collective's Work): the strips are valid, and `strip` may be overwritten,
     only after Work.wait() (for RCCL that makes the caller's current stream
-    wait for the collective, without blocking the host)."""
+    wait for the collective, without blocking the host).  `group`: a process
+    group over all ranks (rank numbers as in the default group), or None."""
     import torch.distributed as dist
 
     if world == 1 and not (dist.is_available() and dist.is_initialized()):  # no process group: nothing to gather
         return ([strip], None) if async_op else [strip]
     bufs = [strip.new_empty(strip.shape) for _ in range(world)] if rank == dst else None
-    work = dist.gather(strip, gather_list=bufs, dst=dst, async_op=async_op)
+    work = dist.gather(strip, gather_list=bufs, dst=dst, async_op=async_op, group=group)
     return (bufs, work) if async_op else bufs
 
 

@@ -145,23 +145,31 @@ def collective(name, fn, *a, **kw):
         raise CollectiveError(f"{name}: {type(e).__name__}: {str(e).splitlines()[0] if str(e) else ''}") from e
 
 
+class stdout_to_stderr:
+    """The process's fd 1 pointed at fd 2 meanwhile: a backend's own start-up
+    chatter (gloo prints its peer connections to stdout from C++) must not
+    reach stdout, which carries only the JSON line."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def init_group(dist, backend, **kw):
-    """init_process_group with the process's fd 1 pointed at fd 2 meanwhile:
-    a backend's own start-up chatter (gloo prints its peer connections to
-    stdout from C++) must not reach stdout, which carries only the JSON line.
-    Every collective of the group times out after DIST_TIMEOUT_S."""
+    """init_process_group with stdout quiet (stdout_to_stderr); every
+    collective of the group times out after DIST_TIMEOUT_S."""
     from datetime import timedelta
 
-    sys.stdout.flush()
-    saved = os.dup(1)
-    try:
-        os.dup2(2, 1)
+    with stdout_to_stderr():
         collective("init_process_group", dist.init_process_group, backend,
                    timeout=timedelta(seconds=DIST_TIMEOUT_S), **kw)
-    finally:
-        sys.stdout.flush()
-        os.dup2(saved, 1)
-        os.close(saved)
 
 
 def dist_setup(torch, dist):
@@ -210,17 +218,20 @@ STUB = os.environ.get("RTMI_BENCH_STUB") == "1"
 # RCCL rehearsal of the exact calls the N-GPU run makes on one GPU; RCCL
 # refuses two ranks on one device).  The line says so (config.dist_rehearsal).
 FORCE_DIST = os.environ.get("RTMI_DIST_FORCE") == "1" and "WORLD_SIZE" in os.environ
-# Where a timed step's gather runs (A/B knob RTMI_BENCH_GATHER=inline|side):
-# "side" issues it as an async collective (torch's NCCL stream, joined by a
-# stream wait before its buffer is rendered into again); "inline" issues it
-# as a synchronous collective, which this torch runs on the caller's current
-# stream: the render's own stream and hardware queue, after the render.  With
-# two contexts that puts one communicator's collectives on two streams, whose
-# kernels may then run out of issue order (NCCL forbids it: a possible hang at
-# N > 1), so "inline" is an A/B mode for one-rank runs only (main() refuses it
-# otherwise).  Measured at one rank (profiles/r06/rccl_one_rank/): 1/8 strip
-# 2.58 (inline) vs 2.66 (side) vs 2.53 ms without gathers.
-GATHER_INLINE = os.environ.get("RTMI_BENCH_GATHER", "side") == "inline"
+# Where a timed step's gather runs (RTMI_BENCH_GATHER=inline|side).
+# "inline" (the default) issues it as a synchronous collective, which this
+# torch runs on the caller's current stream — the render's own stream and
+# hardware queue, right after the render — over a process group of that
+# context's own: one communicator per stream (NCCL forbids one communicator's
+# collectives on two streams, whose kernels could then run out of issue
+# order).  "side" issues it as an async collective of the default group on
+# torch's NCCL stream, joined by a stream wait before its buffer is rendered
+# into again: the cross-stream waits between a context's renders cost the
+# overlap of consecutive launches.  One-rank RCCL run
+# (profiles/r06/rccl_one_rank/ab_gather_mode2.txt): one rank's 1/8 strip 2.60-2.62
+# (inline) vs 2.69 (side) vs 2.54-2.55 ms without gathers; the frame 19.00-19.01 vs
+# 19.08-19.12 vs 18.98-18.99.
+GATHER_INLINE = os.environ.get("RTMI_BENCH_GATHER", "inline") == "inline"
 DIST_REHEARSAL = ("RTMI_DIST_FORCE: one rank through every collective of the N > 1 path (gathers, barriers, max "
                   "over ranks, gather check, one-shot)")
 STALL_RANK = int(os.environ.get("RTMI_BENCH_STALL_RANK", "-1")) if STUB else -1
@@ -651,11 +662,16 @@ def main():
     from a_dive_into_ray_tracing_amd import dist as rdist
 
     world_size, rank, local_rank, dev, coll = dist_setup(torch, dist)
+    from datetime import timedelta
     N = world_size
     DIST = N > 1 or FORCE_DIST  # the N > 1 path: process group, gathers, barriers, max over ranks
-    if GATHER_INLINE and N > 1 and args.pipeline > 1:
-        sys.exit("bench: RTMI_BENCH_GATHER=inline with --pipeline > 1 is a one-rank A/B mode (one communicator on "
-                 "two streams may hang at N > 1)")
+    # inline gathers: one process group (communicator) per context, created
+    # in the same order on every rank
+    ctx_groups = [None] * args.pipeline
+    if DIST and GATHER_INLINE:
+        with stdout_to_stderr():
+            ctx_groups = [collective(f"new_group for context {c}", dist.new_group, list(range(N)),
+                                     timeout=timedelta(seconds=DIST_TIMEOUT_S)) for c in range(args.pipeline)]
 
     world = rt.random_scene()
     cam = rt.final_camera(W / H)
@@ -758,7 +774,8 @@ def main():
         if DIST:  # the single exchange step: strips -> rank 0 over RCCL/xGMI, overlapping the next render
             src = buf if coll.type == dev.type else buf.cpu()  # (gloo rehearsal: host copy)
             if GATHER_INLINE:
-                gathered = collective(f"gather of step {nstep[0]}'s strips", rdist.gather_strips, src, rank, N, dst=0)
+                gathered = collective(f"gather of step {nstep[0]}'s strips", rdist.gather_strips, src, rank, N, dst=0,
+                                      group=ctx_groups[c])
             else:
                 bufs, work = collective(f"gather of step {nstep[0]}'s strips", rdist.gather_strips, src, rank, N,
                                         dst=0, async_op=True)
@@ -831,11 +848,17 @@ def main():
         every = np.array([e.cpu().numpy() for e in every])
         total_segs = float(every[:, 2].sum())
         kernel_ms_max = float(every[:, 0].max())
+        if not GATHER_INLINE:
+            gather_note = "timed steps overlap step k's gather with step k+1's render (strip buffers per context)"
+        elif npipe > 1:
+            gather_note = ("timed steps: step k's gather runs on its context's stream right after its render, over "
+                           "that context's process group, while step k+1 renders on the other context")
+        else:
+            gather_note = "timed steps: step k's gather runs on the render stream between renders k and k+1"
         dist_info = {"backend": str(dist.get_backend()), "world_size": dist.get_world_size(),
                      "kernel_ms_per_rank": [round(float(x), 3) for x in every[:, 0]],
                      "gather_ms_per_rank": [round(float(x), 3) for x in every[:, 1]],
-                     "gather_note": ("timed steps overlap step k's gather with step k+1's render (two strip "
-                                     "buffers); gather_ms is one blocking gather measured after the timed region"),
+                     "gather_note": gather_note + "; gather_ms is one blocking gather measured after the timed region",
                      "segments_per_rank": [int(x) for x in every[:, 2]],
                      "wall_s_per_rank": [round(float(x), 4) for x in every[:, 3]],
                      "kernel_imbalance": round(float(every[:, 0].max() / every[:, 0].mean()), 4)}
@@ -1041,6 +1064,8 @@ def main():
                 "accel": args.accel,
                 "ordering": args.ordering,
                 "pipeline": npipe,
+                **({"gather": ("inline: on each context's stream, one process group per context" if GATHER_INLINE
+                               else "side: async on the default group's NCCL stream")} if DIST else {}),
                 "overlap_schedule": bool(npipe > 1 and args.steps >= 8 and not STUB),
                 "timed_steps": ("each step re-renders the same workload; with ordering 'cost' it dispatches tiles by the "
                                 "previous identical render's per-tile cost map (RT_ORDER_COST): the first render of a "

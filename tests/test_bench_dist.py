@@ -37,6 +37,7 @@ def test_bench_n_ranks_line_schema(n, pipeline, tmp_path):
     assert d["config"]["pipeline"] == pipeline
     assert d["unit"] == "Msamples/s" and d["value"] > 0 and d["ms_per_step"] > 0
     assert d["config"]["partition"] == "interleaved rows, one RCCL gather"
+    assert d["config"]["gather"].startswith("inline")  # per-context process groups (the default)
     di = d["dist"]
     assert di["backend"] == "gloo" and di["world_size"] == n
     for key in ("kernel_ms_per_rank", "gather_ms_per_rank", "segments_per_rank", "wall_s_per_rank"):
@@ -45,7 +46,8 @@ def test_bench_n_ranks_line_schema(n, pipeline, tmp_path):
     # (800 rows are ragged over 3 ranks: padded strips count nothing)
     assert sum(di["segments_per_rank"]) == 1200 * 800 * 500
     assert di["kernel_imbalance"] >= 1.0
-    assert "overlap" in di["gather_note"]  # timed steps: gather k overlaps render k+1 (two buffers)
+    # timed steps: gather k on its context's stream, render k+1 on the other's
+    assert ("while step k+1 renders on the other context" if pipeline > 1 else "between renders k and k+1") in di["gather_note"]
     gc = d["gather_check"]
     assert gc["rows"] == 800 and gc["bit_exact_vs_1gpu_frame"] is True and gc["max_abs_diff"] == 0.0
     assert "cpu_baseline" not in d  # rank 0 at N = 1 only
@@ -122,12 +124,18 @@ def test_force_without_launcher_is_the_plain_path(tmp_path):
     assert "dist" not in d and "dist_rehearsal" not in d["config"] and d["config"]["partition"] == "single GPU"
 
 
-def test_inline_gather_refused_with_two_contexts_at_n_ranks(tmp_path):
-    """RTMI_BENCH_GATHER=inline would put one communicator's gathers on two
-    streams at N > 1 (a possible hang): refused before any rank renders."""
+
+@pytest.mark.parametrize("n,mode", [(2, "side"), (3, "side")])
+def test_side_gathers(n, mode, tmp_path):
+    """RTMI_BENCH_GATHER=side: the gathers as async collectives of the default
+    group (the default, inline, is what test_bench_n_ranks_line_schema runs);
+    the line and the gather check are the same."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
-    env.update(RTMI_DIST_BACKEND="gloo", RTMI_BENCH_STUB="1", OMP_NUM_THREADS="1", RTMI_BENCH_GATHER="inline")
-    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1"],
+    env.update(RTMI_DIST_BACKEND="gloo", RTMI_BENCH_STUB="1", OMP_NUM_THREADS="1", RTMI_BENCH_GATHER=mode)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--steps", "3", "--warmup", "1"],
                        capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
-    assert p.returncode != 0 and p.stdout.strip() == ""
-    assert "one-rank A/B mode" in p.stderr, p.stderr[-2000:]
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads(p.stdout.splitlines()[-1])
+    assert d["config"]["gather"].startswith("side")
+    assert d["dist"]["world_size"] == n and sum(d["dist"]["segments_per_rank"]) == 1200 * 800 * 500
+    assert d["gather_check"]["bit_exact_vs_1gpu_frame"] is True

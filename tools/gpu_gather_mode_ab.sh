@@ -1,8 +1,8 @@
 #!/bin/bash
 # Where the timed steps' gathers run (bench.py's N > 1 path as a one-rank RCCL
 # run, RTMI_DIST_FORCE=1): async on torch's NCCL stream ("side", with the
-# default 4 hardware queues and with 8) against synchronous on the render's own
-# stream ("inline"), frame and 1/8 strip, interleaved REPS times, with the plain
+# default 4 hardware queues; round 6 also ran it with 8) against synchronous on the render's own
+# stream over a process group per context ("inline"), frame and 1/8 strip, interleaved REPS times, with the plain
 # single-GPU line beside them.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -23,7 +23,6 @@ for rep in $(seq ${REPS:-2}); do
     sa=""; [ $so -gt 1 ] && sa="--strip-of $so"
     one plain_s${so}_$rep RTMI_DIST_FORCE=0 -- $sa || exit 1
     one side_s${so}_$rep RTMI_DIST_FORCE=1 -- $sa || exit 1
-    one side_q8_s${so}_$rep RTMI_DIST_FORCE=1 GPU_MAX_HW_QUEUES=8 -- $sa || exit 1
     one inline_s${so}_$rep RTMI_DIST_FORCE=1 RTMI_BENCH_GATHER=inline -- $sa || exit 1
   done
 done

@@ -638,9 +638,12 @@ def main():
                     help="analysis only: render create_world case 1..8 at the nw_* workload's size instead")
     ap.add_argument("--nw-accel", choices=["auto", "bvh", "grid"], default="auto",
                     help="closest-hit structure of the nw_* workloads (rt_nw_ctx_set_accel; same image)")
-    ap.add_argument("--pipeline", type=int, choices=[1, 2, 3], default=2,
+    ap.add_argument("--pipeline", type=int, choices=[1, 2, 3], default=0,
                     help="render contexts the steps alternate over, each on its own hardware queue (2: consecutive "
-                         "steps' renders may overlap; 1: one context, one stream)")
+                         "steps' renders may overlap; 1: one context, one stream).  Default: 2, or 3 when the steps "
+                         "gather (N > 1): a context's gather then sits between its renders, and a third context "
+                         "keeps two renders in flight meanwhile (one-rank RCCL run, 1/8 strip 2.60 -> 2.57 ms; "
+                         "profiles/r06/rccl_one_rank/ab_pipeline3.txt)")
     ap.add_argument("--strip-of", type=int, default=0,
                     help="analysis only: time ONE rank's interleaved strip of an N-GPU run on this GPU")
     args = ap.parse_args()
@@ -665,6 +668,8 @@ def main():
     from datetime import timedelta
     N = world_size
     DIST = N > 1 or FORCE_DIST  # the N > 1 path: process group, gathers, barriers, max over ranks
+    if not args.pipeline:
+        args.pipeline = 3 if DIST else 2
     # inline gathers: one process group (communicator) per context, created
     # in the same order on every rank
     ctx_groups = [None] * args.pipeline

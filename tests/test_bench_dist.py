@@ -17,15 +17,18 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("n,pipeline", [(2, 2), (3, 2), (2, 1), (8, 2)])
+@pytest.mark.parametrize("n,pipeline", [(2, None), (3, 2), (2, 1), (8, None)])
 def test_bench_n_ranks_line_schema(n, pipeline, tmp_path):
-    """pipeline 2 (the default): the steps alternate over two render contexts
-    and two strip buffers; 3 timed steps reuse a buffer after its gather."""
+    """The steps alternate over the render contexts (3 by default when they
+    gather, each with two strip buffers); 7 timed steps reuse buffers after
+    their gathers."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     env.update(RTMI_DIST_BACKEND="gloo", RTMI_BENCH_STUB="1", OMP_NUM_THREADS="1")
-    steps = 3
+    steps = 7
+    pa = ["--pipeline", str(pipeline)] if pipeline else []
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--steps", str(steps), "--warmup", "1",
-                        "--pipeline", str(pipeline)], capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+                        *pa], capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    pipeline = pipeline or 3
     assert p.returncode == 0, p.stderr[-3000:]
     lines = p.stdout.splitlines()
     # rank 0 prints ONE line and nothing else reaches stdout (gloo's start-up

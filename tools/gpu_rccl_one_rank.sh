@@ -23,5 +23,5 @@ print(sys.argv[1], d["value"], d["ms_per_step"], di.get("backend"), di.get("worl
       d["config"].get("pipeline"), d["config"].get("dist_rehearsal") is not None)
 PY
 }
-run p2 --steps 20 --warmup 5 && run p1 --steps 10 --warmup 2 --pipeline 1 &&
+run default --steps 20 --warmup 5 && run p2 --steps 20 --warmup 5 --pipeline 2 && run p1 --steps 10 --warmup 2 --pipeline 1 &&
   run nw --workload nw_motion_blur --nw-spp 50 --steps 3 --warmup 1

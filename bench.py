@@ -11,12 +11,15 @@ j % N), each rank renders its strip on its own GPU, and the strips are
 gathered to rank 0 with ONE RCCL gather (torch.distributed "nccl" = RCCL)
 inside the timed region.  Total work is fixed as N grows: scaling "strong".
 value = W*H*spp*K / max-over-ranks(wall time of K steps) / 1e6.
-Steps alternate over two render contexts, each on a HIP stream with a
-hardware queue of its own (--pipeline 2, the default): step k+1's render is
+Steps alternate over render contexts, each on a HIP stream with a hardware
+queue of its own (--pipeline; 2 by default, 3 at N > 1): step k+1's render is
 independent of step k's, so its first blocks fill the CUs that step k's last
-blocks leave idle (the end-of-dispatch drain).  Every step still
-renders the whole workload; --pipeline 1 runs them one after another on one
-context.
+blocks leave idle (the end-of-dispatch drain).  At N > 1 each
+step's gather runs on its context's stream right after the render, over a
+process group of that context's own.  Every step still renders the whole
+workload; --pipeline 1 runs them one after another on one context.
+RTMI_DIST_FORCE=1 under a launcher runs the N > 1 path at world size 1 (a
+one-rank RCCL rehearsal).
 `--gpus N` without a launcher environment starts the N ranks itself (a
 torch.distributed.run child of a parent that never touches the GPU) and
 refuses to run when fewer than N GPUs are visible.  After the timed region

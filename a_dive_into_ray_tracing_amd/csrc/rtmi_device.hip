@@ -641,63 +641,6 @@ __global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, GridShape<ACC != 0
   }
 }
 
-// ---------------------------------------------------------------------------
-// cost probe kernel
-// ---------------------------------------------------------------------------
-// world.hit calls per tile for the tile ordering of a render with no cost map:
-// one sample (sample 0's key) of 16 of each tile's 64 pixels (every other
-// column and row), paths cut at a.max_depth (the probe depth), four tiles per
-// wave — a quarter of the waves of a 1-spp render of the rows, so a frame's
-// probe is one round of waves.  Only the tiles' counts are written
-// (a.tile_cost, by tile index); the image is the render's alone.
-// (4 waves per SIMD: a frame's probe is 3 750 waves, under the 4 096 slots, and
-// the path loop gets the registers it needs without spilling)
-template <int TW, int ACC>
-__global__ __launch_bounds__(64 * GridShape<ACC != 0>::waves, 4) void probe_kernel(
-    const float4 *__restrict__ geom, const float4 *__restrict__ sh0, const float4 *__restrict__ sh1,
-    const SpherePair *__restrict__ pairs, RenderArgs a, unsigned long long *__restrict__ segments) {
-  constexpr int TH = 64 / TW;
-  constexpr int WPB = GridShape<ACC != 0>::waves;
-  // the 16 probed pixels of a tile: a (TW / SX) x (TH / SY) lattice
-  constexpr int SX = TW == 64 ? 4 : 2, SY = TH == 1 ? 1 : 2, COLS = TW / SX;
-  static_assert(COLS * (TH / SY) == 16, "16 probed pixels per tile");
-  __shared__ float cam_lds[21];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  stage_camera(cam_lds, a);
-  if constexpr (ACC == 0) __syncthreads();  // (accelerated kernels: stage_* ends with one)
-  if constexpr (ACC == 1) stage_bvh(a.acc);
-  else if constexpr (acc_gmem(ACC)) stage_grid_desc(a.acc);
-  else if constexpr (ACC >= 2) stage_grid(a.acc);
-  const int tile = (int(blockIdx.x) * WPB + wave) * 4 + (lane >> 4);
-  const int k = lane & 15;
-  const int lx = SX * (k % COLS), ly = SY * (k / COLS);
-  const int ty = tile / max(a.tiles_x, 1), tx = tile - ty * a.tiles_x;
-  const int x = tx * TW + lx, y = ty * TH + ly;
-  bool active = tile < a.tiles && x < a.W && y < a.nrows_valid;
-  const SceneView<float> sc{geom, sh0, sh1, a.n};
-  SegCounters cnt{};
-  V3<float> o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f), T = mk(1.f, 1.f, 1.f);
-  int pxd = 0;
-  Xoro rng;
-  unsigned nseg = 0;
-  if (active) {
-    const int j = a.row0 + y * a.row_step;
-    rng.init(a.seed, uint64_t(j) * uint64_t(a.W) + uint64_t(x), uint32_t(a.s_base));
-    float ju, jv;
-    rng.pair(ju, jv);
-    get_ray<true, float>(lds_camera(cam_lds), (float(x) + ju) * cam_lds[19], (float(j) + jv) * cam_lds[20], rng, o, d);
-  }
-  while (active) {
-    V3<float> col;
-    ++nseg;
-    if (path_segment<ACC>(sc, pairs, a, o, d, T, pxd, rng, col, cnt, segments)) active = false;
-  }
-  // the tile's 16 lanes summed, one global add per tile
-  for (int m = 8; m >= 1; m >>= 1) nseg += unsigned(__shfl_xor(int(nseg), m, 64));
-  if (k == 0 && tile < a.tiles && a.tile_cost) atomicAdd(&a.tile_cost[tile], nseg);
-}
-
 #if RTMI_EXPERIMENTAL
 // ---------------------------------------------------------------------------
 // resident grid kernel (RT_KERNEL_RESIDENT; experimental
@@ -1370,10 +1313,6 @@ struct rt_ctx {
   // one-shot 2.81 ms with 1 spp to depth 8 against 2.96 with 2 spp to depth
   // 50; the frame 19.57 vs 19.64; profiles/r06/oneshot/)
   int32_t probe_depth = std::getenv("RTMI_PROBE_DEPTH") ? std::atoi(std::getenv("RTMI_PROBE_DEPTH")) : 0;
-  // the probe's kernel (RTMI_PROBE_KIND, for A/B): 1 = probe_kernel (16 pixels
-  // of each tile, 4 tiles per wave; counts only), 0 = a render of the rows at
-  // probe_spp samples into the output strip
-  int32_t probe_kind = std::getenv("RTMI_PROBE_KIND") ? std::atoi(std::getenv("RTMI_PROBE_KIND")) : 1;
   bool probing = false;
   // automatic item size of the grid kernel: ~want_items items of item_min..125
   // samples; 0 = the default of the launch mode below (RTMI_WANT_ITEMS /
@@ -2034,29 +1973,6 @@ void launch_resident(int acc, dim3 grid, size_t lds, hipStream_t st, const rt_ct
 
 #endif  // RTMI_EXPERIMENTAL
 
-// the cost probe (probe_kernel): 4 tiles per wave
-template <int TW>
-void launch_probe(int acc, hipStream_t st, const rt_ctx *ctx, const RenderArgs &a) {
-  RenderArgs b = a;
-  b.acc_off = int32_t((accel_lds_bytes(a.acc, acc) + 15) / 16 * 16);
-#define RTMI_GO(K)                                                                                              \
-  {                                                                                                             \
-    constexpr int wpb = GridShape<(K) != 0>::waves;                                                             \
-    const dim3 grid(unsigned((int64_t(a.tiles) + 4 * wpb - 1) / (4 * wpb)));                                    \
-    hipLaunchKernelGGL((probe_kernel<TW, K>), grid, dim3(64 * wpb), size_t(b.acc_off), st, ctx->geom, ctx->sh0, \
-                       ctx->sh1, ctx->pairs, b, ctx->segments);                                                 \
-  }
-  switch (acc) {
-    case 0: RTMI_GO(0); break;
-    case 1: RTMI_GO(1); break;
-    case 2: RTMI_GO(2); break;
-    case 3: RTMI_GO(3); break;
-    case 4: RTMI_GO(4); break;
-    default: RTMI_GO(5); break;
-  }
-#undef RTMI_GO
-}
-
 template <int TW>
 void launch_shape(bool persistent, int acc, bool chunked, dim3 grid, hipStream_t st, const rt_ctx *ctx,
                   const RenderArgs &a, unsigned long long *accum, float *out) {
@@ -2283,16 +2199,6 @@ int render_rows_impl(rt_ctx *ctx, const rt_camera *cam, int32_t W, int32_t H, in
     std::swap(ctx->cost_prev, ctx->cost_cur);  // this launch's counts order the next one
     std::copy(key, key + 6, ctx->cost_key);
     ctx->cost_valid = true;
-  }
-  if (ctx->probing && ctx->probe_kind == 1) {  // the probe's own kernel: the tiles' counts only
-    switch (TW) {
-      case 8: launch_probe<8>(acc_kind, st, ctx, a); break;
-      case 16: launch_probe<16>(acc_kind, st, ctx, a); break;
-      case 32: launch_probe<32>(acc_kind, st, ctx, a); break;
-      default: launch_probe<64>(acc_kind, st, ctx, a); break;
-    }
-    HIP_TRY(hipGetLastError());
-    return RT_OK;
   }
   // (cleared here, after the cost probe, which may render into the same
   // accumulator)

@@ -1,6 +1,6 @@
 """One-shot render time (the cost probe included) of config 2 and of one
-rank's 1/8 strip, for the probe settings in the environment (RTMI_PROBE_KIND,
-RTMI_PROBE_DEPTH, RTMI_PROBE_SPP; analysis only): K renders each forgetting the cost map, and a
+rank's 1/8 strip, for the probe settings in the environment (RTMI_PROBE_DEPTH,
+RTMI_PROBE_SPP; analysis only): K renders each forgetting the cost map, and a
 steady render (the previous render's map) for reference; prints one JSON
 line of medians (HIP events around each render on its stream)."""
 import json
@@ -21,8 +21,7 @@ r = rt.Renderer(rt.random_scene(), 0)
 r.set_accel("grid")
 cam = rt.final_camera(W / H)
 s = torch.cuda.Stream()
-out = {"probe_kind": os.environ.get("RTMI_PROBE_KIND", "1"), "probe_depth": os.environ.get("RTMI_PROBE_DEPTH", "0"),
-       "probe_spp": os.environ.get("RTMI_PROBE_SPP", "0")}
+out = {"probe_depth": os.environ.get("RTMI_PROBE_DEPTH", "0"), "probe_spp": os.environ.get("RTMI_PROBE_SPP", "0")}
 for name, strip_of in (("frame", 1), ("strip8", 8)):
     row0, step, nrows = rdist.strip_rows(H, 0, strip_of)
     buf = torch.empty((nrows, W, 3), dtype=torch.float32, device="cuda:0")

@@ -21,6 +21,7 @@ VARIANTS = {
     "trace": ("variant", "-DRTMI_TRACE=1 -DRTMI_TRACE_PHASES=1"),  # per-wave timeline + phase clocks (tools/trace_run.py)
     "wavetrace": ("variant", "-DRTMI_TRACE=1"),  # per-wave timeline only (tools/gpu_trace_ab.sh)
     "nwph": ("nwvariant", "-DRTMI_NW_PHASES=1"),  # Next-Week phase clocks (tools/nw_phases.py)
+    "w2": ("variant", "-DRTMI_BVH_WAVES=2"),  # 2-wave grid-kernel blocks (tools/gpu_small_blocks.sh)
 }
 
 

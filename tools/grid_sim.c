@@ -24,6 +24,7 @@
  * sphere) pairs over all 64 lanes.
  *
  *   gcc -O2 -o /tmp/grid_sim tools/grid_sim.c -lm && /tmp/grid_sim tests/golden/scene_final.txt [spp] [stride]
+ *   (BEHIND_CULL=1: candidates without the spheres a ray leaves from outside, as RTMI_BEHIND_CULL)
  */
 #include <math.h>
 #include <stdio.h>
@@ -31,6 +32,7 @@
 #include <string.h>
 
 #define MAXS 1024
+static int g_behind_cull;
 static int N;
 static double C[MAXS][4];
 static int KIND[MAXS];
@@ -159,6 +161,9 @@ static int walk(const Ray *r, int *lens, int *entry_cell) {
       double hb = oc[0]*r->d[0]+oc[1]*r->d[1]+oc[2]*r->d[2];
       double cc = oc[0]*oc[0]+oc[1]*oc[1]+oc[2]*oc[2]-C[q][3]*C[q][3];
       double disc = hb*hb - a*cc; if (disc < 0) continue;
+      /* BEHIND_CULL=1: a sphere the ray leaves from outside (hb > 0, |oc|^2 >= r^2; the bounce origin sits on the
+       * surface here, so |oc|^2 - r^2 >= -1e-9) is no candidate (the kernels' RTMI_BEHIND_CULL) */
+      if (g_behind_cull && hb > 0 && cc >= -1e-9) continue;
       int pos = i - cell_start[cell]; if (pos < 64) g_cand[nc-1] |= 1ull << pos;
       double sq = sqrt(disc), rt = (-hb-sq)/a;
       if (rt < 0.001 || rt > tmax) { rt = (-hb+sq)/a; if (rt < 0.001 || rt > tmax) continue; }
@@ -410,6 +415,7 @@ static void queue_model(int P, int NB, const double *Es, int nE) {
 }
 
 int main(int argc, char **argv) {
+  if (getenv("BEHIND_CULL")) g_behind_cull = atoi(getenv("BEHIND_CULL"));
   FILE *f = fopen(argc > 1 ? argv[1] : "tests/golden/scene_final.txt", "r");
   if (!f || fscanf(f, "%d", &N) != 1) return 1;
   for (int k = 0; k < N; k++)

@@ -22,6 +22,10 @@ VARIANTS = {
     "wavetrace": ("variant", "-DRTMI_TRACE=1"),  # per-wave timeline only (tools/gpu_trace_ab.sh)
     "nwph": ("nwvariant", "-DRTMI_NW_PHASES=1"),  # Next-Week phase clocks (tools/nw_phases.py)
     "w2": ("variant", "-DRTMI_BVH_WAVES=2"),  # 2-wave grid-kernel blocks (tools/gpu_small_blocks.sh)
+    # compiler options for the device code (tools/gpu_variant_ab.sh)
+    "f_prio": ("variant", "-mllvm -amdgpu-set-wave-priority"),
+    "f_trk": ("variant", "-mllvm -amdgpu-use-amdgpu-trackers"),
+
 }
 
 

@@ -119,3 +119,65 @@ def test_cli_checkpoint_requires_pass_spp(tmp_path):
         pytest.skip("CLI not built")
     r = subprocess.run([CLI, "--checkpoint", str(tmp_path / "c")], capture_output=True, text=True)
     assert r.returncode == 2
+
+
+def _read(path, cap):
+    L = _abi.load()
+    n = C.c_int32()
+    g, m, k = np.zeros(4 * cap), np.zeros(4 * cap), np.zeros(cap, np.int32)
+    rc = L.rt_scene_read(str(path).encode(), rt._d(g), k.ctypes.data_as(rt._ip), rt._d(m), cap, C.byref(n))
+    return rc, n.value, g.reshape(cap, 4), k, m.reshape(cap, 4)
+
+
+def test_scene_file_parser_fuzz(tmp_path):
+    """Mutations of the fixture file (lines dropped, duplicated or cut, fields
+    replaced by junk, long lines, stray bytes) and random blobs: rt_scene_read
+    returns RT_OK with a scene that satisfies the reader's own contract (finite,
+    non-zero radii, known materials, within the cap) or RT_EINVAL with a
+    message — never a crash, a hang or an out-of-range write (the arrays are
+    sized to the cap).  Seeded, so the run is reproducible."""
+    hyp = pytest.importorskip("hypothesis")
+    st = hyp.strategies
+    base = open(os.path.join(GOLD, "scene_final.txt")).read().splitlines()
+    junk = st.sampled_from(["", "x", "nan", "inf", "-inf", "1e400", "-0", "0x10", "3", "9" * 400, "\x00", "é", "#", "1 2"])
+
+    @st.composite
+    def mutated(draw):
+        lines = list(base[: draw(st.integers(0, len(base)))])
+        for _ in range(draw(st.integers(0, 6))):
+            if not lines:
+                break
+            i = draw(st.integers(0, len(lines) - 1))
+            op = draw(st.integers(0, 4))
+            if op == 0:
+                del lines[i]
+            elif op == 1:
+                lines.insert(i, lines[i])
+            elif op == 2:
+                lines[i] = lines[i][: draw(st.integers(0, len(lines[i])))]
+            elif op == 3:
+                f = lines[i].split()
+                if f:
+                    f[draw(st.integers(0, len(f) - 1))] = draw(junk)
+                lines[i] = " ".join(f)
+            else:
+                lines[i] = lines[i] + " " + draw(junk)
+        return "\n".join(lines).encode("utf-8", "surrogatepass")
+
+    p = tmp_path / "fuzz.txt"
+    cap = 600
+
+    @hyp.settings(max_examples=150, deadline=None, derandomize=True, database=None)
+    @hyp.given(st.one_of(mutated(), st.binary(max_size=2048)))
+    def check(blob):
+        p.write_bytes(blob)
+        rc, n, g, k, m = _read(p, cap)
+        assert rc in (0, -1), rc
+        if rc == 0:
+            assert 0 <= n <= cap
+            assert np.isfinite(g[:n]).all() and (g[:n, 3] != 0).all()
+            assert set(np.unique(k[:n])) <= {0, 1, 2}
+        else:
+            assert _abi.load().rt_last_error()
+
+    check()
